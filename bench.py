@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: op_mm_quantize (fp32 X[M,K] @ fp32 W[K,N] -> fp32 O via absmax int8).
+
+One "step" = one full drop-in call on inputs already resident in HBM: pack X (Cx + X_int8), pack W
+(Cw + W_int8^T), int8 MFMA GEMM with the fused dequantize epilogue -- exactly the reference's
+op_quantized_mm chain (op_mm.cuh:67-101), which re-quantizes both operands every call.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched under
+torch.distributed.run, one rank per GPU.  Each rank owns its own M-shard (weak scaling over batched
+M: every rank runs the BASELINE configs[1] problem, M=N=K=4096, on its own rows with the replicated
+W); no data-path collective.  Timed region: barrier + synchronize, K steps, synchronize + barrier,
+max over ranks.  Rank 0 prints ONE JSON line.
+
+Extra objects on that line:
+  roofline     -- the dominant kernel (the int8 GEMM): algorithmic 2*M*N*K int8 ops per launch over
+                  its average launch time, measured with HIP events around each GEMM launch inside
+                  the timed region, against the gfx950 dense int8 MFMA peak.
+  cpu_baseline -- the CPU oracle (a C restatement of the reference chain, oracle/) timed on a bounded
+                  row sample of the same workload on the host cores (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+# gfx950 dense int8 MFMA peak: 256 CU x 4 SIMD x 2048 ops/clk (v_mfma_i32_32x32x32_i8: 65536 ops per
+# 32 cycles) x 2.4 GHz = 5.033e15 ops/s (MI355X_MICROARCH.md: i8 = 2x the bf16 2.5 PF dense rate).
+PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12
+PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    # name: (M, N, K, description)  -- BASELINE.json configs
+    "c2": (4096, 4096, 4096, "M=N=K=4096 single-GPU int8 GEMM (BASELINE configs[1])"),
+    "c3_up": (2048, 16384, 4096, "FFN up 2048x4096->16384 (BASELINE configs[2])"),
+    "c3_down": (2048, 4096, 16384, "FFN down 2048x16384->4096 (BASELINE configs[2])"),
+    "c4_shard": (8192, 4096, 4096, "M=65536 K=N=4096 / 8 GPUs, one 8192-row shard (BASELINE configs[3])"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--gather", action="store_true", help="also time the whole-node all-gather of C (N>1)")
+    return p.parse_args()
+
+
+def load_pkg():
+    import _pkg
+    qg = _pkg.package(build=False)
+    qg.load()  # raises if the HIP library is missing: no fallback
+    return qg
+
+
+def cpu_baseline(M, N, K, target_s):
+    """Time the oracle's quantized chain (and the unquantized fp32 GEMM) on a row sample."""
+    import numpy as np
+    from oracle import oracle as O
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    Ms = 16
+    X, W = O.uniform((Ms, K), 0), O.uniform((K, N), 1)
+    t0 = time.perf_counter()
+    O.quantized_mm(X, W)
+    t_cal = time.perf_counter() - t0
+    Ms = int(max(16, min(M, Ms * target_s / max(t_cal, 1e-3))))
+    X = O.uniform((Ms, K), 0)
+    t0 = time.perf_counter()
+    O.quantized_mm(X, W)
+    tq = time.perf_counter() - t0
+    # unquantized fp32 path (op_mm<float,float>), smaller sample
+    Mf = max(4, Ms // 4)
+    t0 = time.perf_counter()
+    O.mm_fp32(X[:Mf], W)
+    tf = time.perf_counter() - t0
+    gemm_s = tq * M / Ms
+    return {
+        "value": 1.0 / gemm_s,
+        "unit": "GEMMs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle quantized chain on {Ms} of {M} rows (N={N}, K={K}), {tq:.1f} s, "
+                  f"linear in rows -> {gemm_s:.1f} s per full GEMM; unquantized fp32 op_mm on {Mf} rows "
+                  f"-> {tf * M / Mf:.1f} s per full GEMM",
+        "unquantized_gemms_per_s": 1.0 / (tf * M / Mf),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if distributed else 0)
+    torch.cuda.set_device(dev)
+
+    qg = load_pkg()
+    L = qg.load()
+    M, N, K, desc = CONFIGS[args.config]
+
+    # inputs resident in HBM before timing; X differs per rank (its M-shard), W is replicated
+    X = qg.fill_uniform(torch.empty((M, K), device=dev), seed=2 * (1000 + rank))
+    W = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 1000 + 1)
+    O = torch.empty((M, N), device=dev)
+    pa = torch.empty(L.qgemm_packed_size(M, K), dtype=torch.uint8, device=dev)
+    pb = torch.empty(L.qgemm_packed_size(N, K), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    s = qg._stream(dev)
+    range_ = 127.0
+
+    def step(ev=None):
+        rc = L.qgemm_pack_a(X.data_ptr(), K, 1, M, K, range_, pa.data_ptr(), s)
+        rc |= L.qgemm_pack_b(W.data_ptr(), N, 1, K, N, range_, pb.data_ptr(), s)
+        if ev is not None:
+            ev[0].record(stream)
+        rc |= L.qgemm_mm_packed(pa.data_ptr(), pb.data_ptr(), O.data_ptr(), N, 1, M, N, K, range_, s)
+        if ev is not None:
+            ev[1].record(stream)
+        if rc:
+            raise RuntimeError(f"qgemm returned {rc}")
+
+    for _ in range(args.warmup):
+        step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    gemm_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    if distributed:
+        t = torch.tensor([elapsed, gemm_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gemm_ms = float(t[0]), float(t[1])
+
+    gather_ms = None
+    if distributed and args.gather:
+        from importlib import import_module  # noqa: F401
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        full = qg.shard.gather_rows(O, M * world)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        del full
+
+    ops = 2.0 * M * N * K
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * args.steps / elapsed
+    achieved = ops / (gemm_ms * 1e-3) / 1e12
+    result = {
+        "metric": "int8 GEMMs/sec + achieved int8-MFMA TOPS%, M=N=K=4096, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "GEMMs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic U(-1,1) fp32 inputs (seeded counter-based generator, generated in HBM)",
+        "config": {
+            "workload": f"op_mm_quantize fp32->fp32, {desc}: pack X + pack W + int8 MFMA GEMM/dequant per step",
+            "M": M, "N": N, "K": K, "global_M": M * world, "range": range_,
+            "parallelism": f"M-shard x{world} (replicated W, no collective)",
+        },
+        "tops_full_path": round(ops * world * args.steps / elapsed / 1e12, 2),
+        "tops_pct_full_path": round(100 * ops * args.steps / elapsed / 1e12 / PEAK_INT8_TOPS, 2),
+        "gemm_kernel_ms": round(gemm_ms, 5),
+        "core_gemms_per_s": round(world * 1e3 / gemm_ms, 2),
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": round(PEAK_INT8_TOPS, 1),
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_INT8_TOPS, 4),
+            "traffic": None,
+            "kernel": "gemm_i8_kernel<true> (int8 MFMA GEMM + dequant epilogue)",
+        },
+        "library": qg.version(),
+    }
+    if gather_ms is not None:
+        result["allgather_C_ms"] = round(gather_ms, 3)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(M, N, K, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

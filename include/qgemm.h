@@ -1,0 +1,102 @@
+/*
+ * qgemm.h -- C-ABI of the MI355X-native (gfx950) int8 absmax quantized GEMM.
+ *
+ * Drop-in for the reference's quantized matrix multiply
+ *     template<typename T> void op_quantized_mm(const Tensor<T>& X, const Tensor<T>& W,
+ *                                               Tensor<T>& O, T range)
+ *     (/root/reference/src/ops/op_mm.cuh:67-101, instantiated only at T = float,
+ *      called from test_quantize.cu:78 and inlined in timing_quantize.cu:38-58)
+ * as the flat C entry point the north star names, op_mm_quantize(A, B, C, M, N, K).
+ *
+ * Semantics (bit-exact with the reference chain, see DESIGN.md "Semantics"):
+ *   Cx[i] = absmax of row i of A with the reference's signed-first-element seed
+ *   Cw[j] = absmax of column j of B, same seed rule
+ *   Aq = trunc_sat_i8(A * fl(range/Cx)), Bq = trunc_sat_i8(B * fl(range/Cw))
+ *   C[i,j] = fl(fl(float(sum_k Aq[i,k]*Bq[k,j]) * (fl(Cx[i]*Cw[j]) + 0)) * fl(1/fl(range*range)))
+ *
+ * Conventions
+ *   - All matrix pointers are DEVICE pointers (the reference asserts on_device, op_mm.cuh:72).
+ *   - Return value: 0 on success, otherwise a hipError_t code (hipErrorInvalidValue = 1 for
+ *     bad shapes / null pointers -- where the reference would assert(), op_mm.cuh:71-72).
+ *   - Work is enqueued asynchronously; the plain entry point uses the null stream, like the
+ *     reference's launches (legacy default stream).
+ *   - No parameter is named N: the reference's op_elemwise.cuh:10 does "#define N 256".
+ *   - Not re-entrant across threads on ONE device with the implicit workspace; pass an explicit
+ *     workspace (op_mm_quantize_ws) for concurrent streams or for hipGraph capture.
+ */
+#ifndef QGEMM_H_
+#define QGEMM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define QGEMM_API __attribute__((visibility("default")))
+#else
+#define QGEMM_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Replaces op_quantized_mm<float>(X, W, O, 127.0f) (op_mm.cuh:67-101).
+ * A = X: m x k, row-major fp32.  B = W: k x n, row-major fp32.  C = O: m x n, row-major fp32. */
+QGEMM_API int op_mm_quantize(const float *A, const float *B, float *C, int m, int n, int k);
+
+/* Strided form: element (r, c) of a matrix lives at ptr[r*stride_h + c*stride_w], exactly the
+ * reference's Index() macro (tensor.cuh:14), so transposed views (tensor.cuh:121-133) work.
+ * range is the reference's `range` argument (127 at every reference call site). stream is a
+ * hipStream_t (NULL = null stream). */
+QGEMM_API int op_mm_quantize_ex(const float *A, int64_t a_stride_h, int64_t a_stride_w,
+                      const float *B, int64_t b_stride_h, int64_t b_stride_w,
+                      float *C, int64_t c_stride_h, int64_t c_stride_w,
+                      int m, int n, int k, float range, void *stream);
+
+/* Same, with caller-owned device workspace (no allocation inside: safe for hipGraph capture and
+ * for concurrent calls on different streams).  ws_bytes >= op_mm_quantize_workspace_size(m,n,k). */
+QGEMM_API size_t op_mm_quantize_workspace_size(int m, int n, int k);
+QGEMM_API int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w,
+                      const float *B, int64_t b_stride_h, int64_t b_stride_w,
+                      float *C, int64_t c_stride_h, int64_t c_stride_w,
+                      int m, int n, int k, float range,
+                      void *workspace, size_t ws_bytes, void *stream);
+
+/* ---- The chain's stages (the reference's L2 primitives, fused MI355X-style) ----------------
+ * Packed operand = the quantized operand in MFMA-ready form, in ONE device buffer:
+ *   [ scale: rows_pad f32 ][ reserved: rows_pad u32 ][ q: rows_pad x k_pad int8, row-major, zero padded ]
+ * rows_pad = round_up(rows, 256), k_pad = round_up(k, 128).  For A, rows = m and the scale is
+ * Cx (op_absmax(X,Cx), op_mm.cuh:76-77) and q = X_int8 (op_mm.cuh:86-87).  For B, rows = n
+ * (B is stored transposed, k contiguous) and the scale is Cw (op_mm.cuh:78-79), q = W_int8^T.
+ * Packing B once and reusing it is the LLM.int8() weight-cache pattern. */
+QGEMM_API size_t qgemm_packed_size(int rows, int k);
+QGEMM_API int qgemm_pack_a(const float *A, int64_t a_stride_h, int64_t a_stride_w, int m, int k, float range,
+                 void *packed_a, void *stream);
+QGEMM_API int qgemm_pack_b(const float *B, int64_t b_stride_h, int64_t b_stride_w, int k, int n, float range,
+                 void *packed_b, void *stream);
+/* int8 x int8 -> int32 MFMA GEMM with the fused dequantize epilogue (op_mm.cuh:92-99). */
+QGEMM_API int qgemm_mm_packed(const void *packed_a, const void *packed_b, float *C, int64_t c_stride_h,
+                    int64_t c_stride_w, int m, int n, int k, float range, void *stream);
+/* Debug/parity view of the raw int32 accumulator (op_mm<int8_t,int>, op_mm.cuh:92-93):
+ * Acc is m x n row-major int32. */
+QGEMM_API int qgemm_mm_packed_i32(const void *packed_a, const void *packed_b, int32_t *Acc, int m, int n, int k,
+                        void *stream);
+
+/* The reference's UNQUANTIZED op_mm<float,float> (op_mm.cuh:49-65), bit-exact: sequential-k fmaf from +0.
+ * Used for the reference's error metric (timing_quantize.cu:67-70) and its unquantized timing line. */
+QGEMM_API int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride_w,
+                  const float *B, int64_t b_stride_h, int64_t b_stride_w,
+                  float *C, int64_t c_stride_h, int64_t c_stride_w, int m, int n, int k, void *stream);
+
+/* Deterministic U[lo,hi) fill, bit-identical to oracle_fill_uniform (stands in for the
+ * reference's cuRAND op_uniform_init, op_elemwise.cuh:728-744). */
+QGEMM_API int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, void *stream);
+
+/* Library identification: "qgemm <version> gfx950 <kernel config>". */
+QGEMM_API const char *qgemm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QGEMM_H_ */

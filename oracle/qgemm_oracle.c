@@ -1,0 +1,333 @@
+/*
+ * qgemm_oracle.c -- CPU restatement of the reference's int8 quantized GEMM chain.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (the HIP library under
+ * quantized-gemm-for-transformer-inference_amd/) links, loads or calls this file.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it,
+ * and only as the checker / the CPU baseline -- never as the thing measured.
+ *
+ * It restates, element for element, the arithmetic of
+ *   /root/reference/src/ops/op_mm.cuh:67-101  op_quantized_mm<float>(X, W, O, range)
+ * as the reference's ten kernel launches perform it (citations per function below).
+ * The reference itself cannot be built here (its headers need cuda_runtime.h /
+ * curand.h, which this image lacks), so this restatement is pinned by the reference's
+ * own fixture (test_quantize.cu:38-62, outputs recorded in SURVEY.md s4 KAT-1) and by
+ * an independent pure-Python literal restatement (oracle/literal.py).  See DESIGN.md
+ * "Oracle".
+ *
+ * Semantics:
+ *   Cx[i] = seed X[i,0], then for k>=1: if |X[i,k]| > acc: acc = |X[i,k]|      (quirk)
+ *   sx[i] = fl(range / Cx[i])                              (IEEE division)
+ *   Xq[i,k] = sat_i8(trunc(fl(X[i,k] * sx[i])))   NaN -> 0  (reference: static_cast)
+ *   Acc[i,j] = sum_k Xq[i,k] * Wq[k,j]                     exact int32
+ *   Outer[i,j] = fl(Cx[i] * Cw[j]) + 0.0f                  (K=1 fp32 op_mm)
+ *   O[i,j] = fl(fl((float)Acc * Outer) * fl(1/fl(range*range)))
+ *
+ * Build: see oracle/Makefile (gcc -O3 -ffp-contract=off -fopenmp, no fast-math).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+#define ORACLE_TILE 32 /* TILE_WIDTH, op_mm.cuh:6 -- sets the zero-padding of the fp32 k loop */
+
+/* ---------------------------------------------------------------------------------
+ * Deterministic input generator (shared bit-for-bit with the HIP fill kernel).
+ * Restates op_uniform_init (op_elemwise.cuh:728-744) on our own counter-based
+ * generator: u in [0,1) with 24 random bits, then t = fl(u + fl(lo/(hi-lo))),
+ * x = fl(t * fl(hi-lo)).  For (lo,hi) = (-1,1) this is exactly 2u-1.
+ * ------------------------------------------------------------------------------- */
+static uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+float oracle_uniform_at(uint64_t seed, uint64_t i, float lo, float hi)
+{
+    uint64_t key = mix64(seed + 0x9E3779B97F4A7C15ULL);
+    uint64_t z = mix64(key + (i + 1) * 0x9E3779B97F4A7C15ULL);
+    float u = (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+    float span = hi - lo;
+    float shift = lo / span;
+    float t = u + shift;
+    return t * span;
+}
+
+void oracle_fill_uniform(float *out, int64_t n, uint64_t seed, float lo, float hi)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = oracle_uniform_at(seed, (uint64_t)i, lo, hi);
+}
+
+/* ---------------------------------------------------------------------------------
+ * AbsMaxFunc (op_reduction.cuh:7-25) applied as the reduction kernels do:
+ * accumulator seeded with the SIGNED first element (colwise :80 / rowwise :105),
+ * then the functor for i >= 1 (:81-83 / :106-108).  Reproduced literally, including
+ * which zero sign survives and that NaN at i>=1 is skipped while a NaN seed sticks.
+ * ------------------------------------------------------------------------------- */
+static inline void absmax_step(float x, float *acc)
+{
+    if (x > 0) {
+        if (x > *acc) *acc = x;
+    } else {
+        if (-x > *acc) *acc = -x;
+    }
+}
+
+/* Cx[i] = AbsMax over row i of X[M x K] (op_absmax(X, Cx), op_mm.cuh:76-77 -> colwise kernel). */
+void oracle_absmax_rows(const float *X, int M, int K, float *Cx)
+{
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < M; ++i) {
+        const float *row = X + (int64_t)i * K;
+        float acc = row[0];
+        for (int k = 1; k < K; ++k) absmax_step(row[k], &acc);
+        Cx[i] = acc;
+    }
+}
+
+/* Cw[j] = AbsMax over column j of W[K x N] (op_absmax(W, Cw), op_mm.cuh:78-79 -> rowwise kernel).
+ * K == 1 is undefined in the reference (it takes the colwise branch and leaves Cw[1..]
+ * uninitialised); we define Cw[j] = W[0,j], the per-column seed. */
+void oracle_absmax_cols(const float *W, int K, int N, float *Cw)
+{
+    for (int j = 0; j < N; ++j) Cw[j] = W[j];
+    for (int k = 1; k < K; ++k) {
+        const float *row = W + (int64_t)k * N;
+        for (int j = 0; j < N; ++j) absmax_step(row[j], &Cw[j]);
+    }
+}
+
+/* InvDivideConstFunc (op_elemwise.cuh:131-143): s = range / C, correctly rounded. */
+void oracle_inv_divide(const float *C, int n, float range, float *s)
+{
+    for (int i = 0; i < n; ++i) s[i] = range / C[i];
+}
+
+/* MultiplyWithTypecastFunc<float,int8_t> (op_elemwise.cuh:106-114): static_cast<int8_t>(x*a).
+ * The cast truncates toward zero; outside [-128,127] (reachable only through the absmax
+ * quirk) and for NaN it is undefined in C++ -- we define saturation and NaN -> 0, the
+ * behaviour of a saturating hardware convert.  Written without UB. */
+static inline int8_t quant_i8(float x, float s)
+{
+    float v = x * s;
+    if (v != v) return 0;
+    if (v >= 127.0f) return 127;
+    if (v <= -128.0f) return -128;
+    return (int8_t)(int)v; /* |v| < 128: truncation, defined */
+}
+
+/* op_multiply(X, sx, X_int8) (op_mm.cuh:86-87): row broadcast of sx (bcast kernel :416-418). */
+void oracle_quantize_rows(const float *X, const float *sx, int M, int K, int8_t *Xq)
+{
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < M; ++i)
+        for (int k = 0; k < K; ++k)
+            Xq[(int64_t)i * K + k] = quant_i8(X[(int64_t)i * K + k], sx[i]);
+}
+
+/* op_multiply(W, sw, W_int8) (op_mm.cuh:88-89): column broadcast of sw (bcast kernel :412-414). */
+void oracle_quantize_cols(const float *W, const float *sw, int K, int N, int8_t *Wq)
+{
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < K; ++k)
+        for (int j = 0; j < N; ++j)
+            Wq[(int64_t)k * N + j] = quant_i8(W[(int64_t)k * N + j], sw[j]);
+}
+
+/* op_mm<int8_t,int>(X_int8, W_int8, O_int32) (op_mm.cuh:92-93 -> op_matmul_kernel :9-46),
+ * restated as the exact int32 dot product.  The reference accumulates through fp32 FMA
+ * (int res; res += (float)a*(float)b, :37-39), identical to this while every partial sum
+ * stays below 2^24 in magnitude; oracle_int8_mm_fp32emu below restates that literally
+ * and the tests check both agree on every input they use. */
+void oracle_int8_mm(const int8_t *Xq, const int8_t *Wq, int M, int N, int K, int32_t *Acc)
+{
+    int8_t *WqT = (int8_t *)malloc((size_t)N * (size_t)K + 1);
+    for (int k = 0; k < K; ++k)
+        for (int j = 0; j < N; ++j) WqT[(int64_t)j * K + k] = Wq[(int64_t)k * N + j];
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int i = 0; i < M; ++i) {
+        const int8_t *a = Xq + (int64_t)i * K;
+        for (int j = 0; j < N; ++j) {
+            const int8_t *b = WqT + (int64_t)j * K;
+            int32_t s = 0;
+            for (int k = 0; k < K; ++k) s += (int16_t)a[k] * (int16_t)b[k];
+            Acc[(int64_t)i * N + j] = s;
+        }
+    }
+    free(WqT);
+}
+
+/* Literal restatement of op_matmul_kernel<int8_t,int>: per 32-wide k tile, res += A*B with
+ * the operands staged as float (op_mm.cuh:16-17) and the += contracted to an fma (nvcc
+ * default), then converted back to int (truncation).  Zero-padded tail products as the
+ * kernel loads them (:21-33).  Slow; small sizes only. */
+void oracle_int8_mm_fp32emu(const int8_t *Xq, const int8_t *Wq, int M, int N, int K, int32_t *Acc)
+{
+    int ntiles = (K - 1) / ORACLE_TILE + 1;
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j) {
+            int res = 0;
+            for (int t = 0; t < ntiles * ORACLE_TILE; ++t) {
+                float a = t < K ? (float)Xq[(int64_t)i * K + t] : 0.0f;
+                float b = t < K ? (float)Wq[(int64_t)t * N + j] : 0.0f;
+                res = (int)fmaf(a, b, (float)res);
+            }
+            Acc[(int64_t)i * N + j] = res;
+        }
+}
+
+/* op_mm<float,float>(Cx, Cw, Outer) with K = 1 (op_mm.cuh:96-97): res = 0, then 32 products
+ * of which 31 are the zero padding; = fl(Cx*Cw) + 0.0f (a -0 product becomes +0). */
+static inline float outer_at(float cx, float cw)
+{
+    float r = fmaf(cx, cw, 0.0f);
+    return r + 0.0f;
+}
+
+/* op_dequantize (op_elemwise.cuh:614-625, DequantizeFunc :93-103) then
+ * op_multiply(O, 1/(range*range), O) (op_mm.cuh:99, MultiplyConstFunc :118-129). */
+static inline float dequant(int32_t acc, float cx, float cw, float inv_r2)
+{
+    float o = (float)acc * outer_at(cx, cw);
+    return o * inv_r2;
+}
+
+void oracle_dequantize(const int32_t *Acc, const float *Cx, const float *Cw, int M, int N,
+                       float range, float *O)
+{
+    float inv_r2 = 1.0f / (range * range);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j)
+            O[(int64_t)i * N + j] = dequant(Acc[(int64_t)i * N + j], Cx[i], Cw[j], inv_r2);
+}
+
+/* Whole chain, op_quantized_mm (op_mm.cuh:67-101).  Optional intermediates (may be NULL). */
+void oracle_quantized_mm_ex(const float *X, const float *W, float *O, int M, int N, int K, float range,
+                            float *Cx_out, float *Cw_out, int8_t *Xq_out, int8_t *Wq_out, int32_t *Acc_out)
+{
+    float *Cx = Cx_out ? Cx_out : (float *)malloc(sizeof(float) * (size_t)M);
+    float *Cw = Cw_out ? Cw_out : (float *)malloc(sizeof(float) * (size_t)N);
+    float *sx = (float *)malloc(sizeof(float) * (size_t)M);
+    float *sw = (float *)malloc(sizeof(float) * (size_t)N);
+    int8_t *Xq = Xq_out ? Xq_out : (int8_t *)malloc((size_t)M * (size_t)K + 1);
+    int8_t *Wq = Wq_out ? Wq_out : (int8_t *)malloc((size_t)K * (size_t)N + 1);
+    int32_t *Acc = Acc_out ? Acc_out : (int32_t *)malloc(sizeof(int32_t) * (size_t)M * (size_t)N);
+
+    oracle_absmax_rows(X, M, K, Cx);
+    oracle_absmax_cols(W, K, N, Cw);
+    oracle_inv_divide(Cx, M, range, sx);
+    oracle_inv_divide(Cw, N, range, sw);
+    oracle_quantize_rows(X, sx, M, K, Xq);
+    oracle_quantize_cols(W, sw, K, N, Wq);
+    oracle_int8_mm(Xq, Wq, M, N, K, Acc);
+    oracle_dequantize(Acc, Cx, Cw, M, N, range, O);
+
+    if (!Cx_out) free(Cx);
+    if (!Cw_out) free(Cw);
+    free(sx);
+    free(sw);
+    if (!Xq_out) free(Xq);
+    if (!Wq_out) free(Wq);
+    if (!Acc_out) free(Acc);
+}
+
+void oracle_quantized_mm(const float *X, const float *W, float *O, int M, int N, int K, float range)
+{
+    oracle_quantized_mm_ex(X, W, O, M, N, K, range, NULL, NULL, NULL, NULL, NULL);
+}
+
+/* The chain for a SUBSET of output rows: rows are independent given Cw, so a full-size
+ * GPU result can be checked bit-exactly on sampled rows in seconds.  O_rows is [nrows x N]. */
+void oracle_quantized_mm_rows(const float *X, const float *W, float *O_rows, int M, int N, int K,
+                              float range, const int *rows, int nrows)
+{
+    (void)M;
+    float *Cw = (float *)malloc(sizeof(float) * (size_t)N);
+    float *sw = (float *)malloc(sizeof(float) * (size_t)N);
+    int8_t *WqT = (int8_t *)malloc((size_t)N * (size_t)K + 1);
+    oracle_absmax_cols(W, K, N, Cw);
+    oracle_inv_divide(Cw, N, range, sw);
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < N; ++j)
+        for (int k = 0; k < K; ++k) WqT[(int64_t)j * K + k] = quant_i8(W[(int64_t)k * N + j], sw[j]);
+    float inv_r2 = 1.0f / (range * range);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; ++r) {
+        const float *x = X + (int64_t)rows[r] * K;
+        float cx;
+        oracle_absmax_rows(x, 1, K, &cx);
+        float sx = range / cx;
+        int8_t *xq = (int8_t *)malloc((size_t)K + 1);
+        for (int k = 0; k < K; ++k) xq[k] = quant_i8(x[k], sx);
+        for (int j = 0; j < N; ++j) {
+            const int8_t *b = WqT + (int64_t)j * K;
+            int32_t s = 0;
+            for (int k = 0; k < K; ++k) s += (int16_t)xq[k] * (int16_t)b[k];
+            O_rows[(int64_t)r * N + j] = dequant(s, cx, Cw[j], inv_r2);
+        }
+        free(xq);
+    }
+    free(Cw);
+    free(sw);
+    free(WqT);
+}
+
+/* op_mm<float,float>(X, W, C) (op_mm.cuh:49-65 -> op_matmul_kernel<float,float>): the
+ * unquantized path.  res starts at +0 and is accumulated sequentially in k with fmaf
+ * (nvcc contracts :38), including the zero-padded products of the last 32-wide tile. */
+void oracle_mm_fp32(const float *X, const float *W, float *C, int M, int N, int K)
+{
+    int kpad = ((K - 1) / ORACLE_TILE + 1) * ORACLE_TILE;
+#pragma omp parallel
+    {
+        float *acc = (float *)malloc(sizeof(float) * (size_t)N);
+#pragma omp for schedule(dynamic, 1)
+        for (int i = 0; i < M; ++i) {
+            for (int j = 0; j < N; ++j) acc[j] = 0.0f;
+            /* i-k-j order: each acc[j] still sees its k terms in ascending order */
+            for (int k = 0; k < K; ++k) {
+                float a = X[(int64_t)i * K + k];
+                const float *w = W + (int64_t)k * N;
+                for (int j = 0; j < N; ++j) acc[j] = fmaf(a, w[j], acc[j]);
+            }
+            for (int k = K; k < kpad; ++k)
+                for (int j = 0; j < N; ++j) acc[j] = fmaf(0.0f, 0.0f, acc[j]);
+            memcpy(C + (int64_t)i * N, acc, sizeof(float) * (size_t)N);
+        }
+        free(acc);
+    }
+}
+
+/* op_subtract(C, qC, err) then err.toHost().mean() (tensor.cuh:201-211): a SIGNED mean,
+ * summed sequentially in fp32 and divided by h*w (an int converted to float). */
+float oracle_signed_mean_error(const float *C, const float *O, int64_t n)
+{
+    float sum = 0.0f;
+    for (int64_t i = 0; i < n; ++i) {
+        float d = C[i] - O[i];
+        sum += d;
+    }
+    return sum / (float)(int)n;
+}
+
+/* Error statistics beyond the reference's metric: mean|E|, max|E|, and sum|C| (for relative). */
+void oracle_error_stats(const float *C, const float *O, int64_t n, double *mean_abs, double *max_abs,
+                        double *mean_abs_ref)
+{
+    double s = 0.0, m = 0.0, r = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        double d = fabs((double)C[i] - (double)O[i]);
+        s += d;
+        if (d > m) m = d;
+        r += fabs((double)C[i]);
+    }
+    *mean_abs = s / (double)n;
+    *max_abs = m;
+    *mean_abs_ref = r / (double)n;
+}

@@ -1,0 +1,266 @@
+"""qgemm_amd -- host-side mirror of the reference's quantized-GEMM operator over the C-ABI.
+
+The product is ``build/libqgemm.so`` (hand-written gfx950 HIP kernels behind the C-ABI in
+``include/qgemm.h``).  This module binds that ABI with ctypes and mirrors the reference's
+operator interface for the hot path:
+
+    op_quantized_mm(X, W, O, range)   <- op_mm.cuh:67-101 (same name, argument meaning, asserts)
+    op_mm_quantize(A, B, C)           <- the north-star C-ABI op_mm_quantize(A,B,C,M,N,K)
+    pack_a / pack_b / mm_packed       <- the chain's stages (op_absmax+op_inv_divide+op_multiply,
+                                         op_mm<int8_t,int>+op_dequantize+op_multiply)
+    fill_uniform                      <- op_uniform_init (op_elemwise.cuh:728-744), seeded
+
+PyTorch is plumbing here: it owns device memory and streams.  There is NO CPU fallback: if the
+HIP library is missing, every compute entry point raises.
+
+Import it by path (the directory name is not a Python identifier)::
+
+    import importlib.util, sys
+    spec = importlib.util.spec_from_file_location("qgemm_amd", "<repo>/quantized-gemm-for-transformer-inference_amd/__init__.py")
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "build", "libqgemm.so")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "qgemm.h")
+
+DEFAULT_RANGE = 127.0  # `range` at every reference call site (test_quantize.cu:76, timing_quantize.cu:43)
+ROW_PAD = 256          # packed operand rows are padded to the GEMM macro-tile
+K_PAD = 128            # packed operand k is padded to the GEMM k-step
+
+# Every symbol include/qgemm.h declares (checked against the header by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "op_mm_quantize",
+    "op_mm_quantize_ex",
+    "op_mm_quantize_workspace_size",
+    "op_mm_quantize_ws",
+    "qgemm_packed_size",
+    "qgemm_pack_a",
+    "qgemm_pack_b",
+    "qgemm_mm_packed",
+    "qgemm_mm_packed_i32",
+    "qgemm_mm_fp32",
+    "qgemm_fill_uniform",
+    "qgemm_version",
+)
+
+HIP_ERROR_INVALID_VALUE = 1
+
+_lock = threading.Lock()
+_lib = None
+
+
+class QGemmError(RuntimeError):
+    """A non-zero hipError_t returned through the C-ABI."""
+
+    def __init__(self, fn: str, code: int):
+        super().__init__(f"{fn} failed with hipError_t {code}")
+        self.code = code
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libqgemm.so and the harness binaries for gfx950 (hipcc; see Makefile)."""
+    out = None if verbose else subprocess.DEVNULL
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-C", PKG_DIR, "-j", jobs, "all"], check=True, stdout=out)
+    return LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library (no fallback: raises if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"qgemm HIP library not built: {LIB_PATH} missing (run build())")
+        L = ctypes.CDLL(LIB_PATH)
+        i64, i32, f32, vp, sz = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+        L.op_mm_quantize.argtypes = [vp, vp, vp, i32, i32, i32]
+        L.op_mm_quantize.restype = i32
+        L.op_mm_quantize_ex.argtypes = [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, f32, vp]
+        L.op_mm_quantize_ex.restype = i32
+        L.op_mm_quantize_workspace_size.argtypes = [i32, i32, i32]
+        L.op_mm_quantize_workspace_size.restype = sz
+        L.op_mm_quantize_ws.argtypes = [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, f32, vp, sz, vp]
+        L.op_mm_quantize_ws.restype = i32
+        L.qgemm_packed_size.argtypes = [i32, i32]
+        L.qgemm_packed_size.restype = sz
+        L.qgemm_pack_a.argtypes = [vp, i64, i64, i32, i32, f32, vp, vp]
+        L.qgemm_pack_a.restype = i32
+        L.qgemm_pack_b.argtypes = [vp, i64, i64, i32, i32, f32, vp, vp]
+        L.qgemm_pack_b.restype = i32
+        L.qgemm_mm_packed.argtypes = [vp, vp, vp, i64, i64, i32, i32, i32, f32, vp]
+        L.qgemm_mm_packed.restype = i32
+        L.qgemm_mm_packed_i32.argtypes = [vp, vp, vp, i32, i32, i32, vp]
+        L.qgemm_mm_packed_i32.restype = i32
+        L.qgemm_mm_fp32.argtypes = [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, vp]
+        L.qgemm_mm_fp32.restype = i32
+        L.qgemm_fill_uniform.argtypes = [vp, i64, ctypes.c_uint64, f32, f32, vp]
+        L.qgemm_fill_uniform.restype = i32
+        L.qgemm_version.argtypes = []
+        L.qgemm_version.restype = ctypes.c_char_p
+        _lib = L
+        return L
+
+
+def version() -> str:
+    return load().qgemm_version().decode()
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != 0:
+        raise QGemmError(fn, rc)
+
+
+def _stream(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_device_f32(t, name):
+    import torch
+    assert isinstance(t, torch.Tensor) and t.dim() == 2, f"{name} must be a 2-D tensor"
+    assert t.is_cuda, f"{name}.on_device (op_mm.cuh:72)"
+    assert t.dtype == torch.float32, f"{name} must be float32 (op_quantized_mm is instantiated at T=float)"
+
+
+# ------------------------------------------------------------------------------- the operator
+def op_quantized_mm(X, W, O, range: float = DEFAULT_RANGE) -> None:  # noqa: A002 - reference name
+    """O = quantized X @ W, in place -- the reference's ``op_quantized_mm<float>`` (op_mm.cuh:67-101).
+
+    Same argument meaning and the same asserts (op_mm.cuh:71-72): ``X.h == O.h && W.w == O.w &&
+    X.w == W.h`` and all three on the device.  Strided/transposed views are accepted, as the
+    reference's Index() macro accepts them.  Enqueued on torch's current stream.
+    """
+    for t, nm in ((X, "X"), (W, "W"), (O, "O")):
+        _require_device_f32(t, nm)
+    assert X.shape[0] == O.shape[0] and W.shape[1] == O.shape[1] and X.shape[1] == W.shape[0], \
+        "X.h == O.h && W.w == O.w && X.w == W.h (op_mm.cuh:71)"
+    M, K = X.shape
+    N = W.shape[1]
+    if M == 0 or N == 0:
+        return
+    rc = load().op_mm_quantize_ex(X.data_ptr(), X.stride(0), X.stride(1), W.data_ptr(), W.stride(0), W.stride(1),
+                                  O.data_ptr(), O.stride(0), O.stride(1), M, N, K, float(range), _stream(X.device))
+    _check("op_mm_quantize_ex", rc)
+
+
+def op_mm_quantize(A, B, C=None):
+    """The north-star C-ABI op_mm_quantize(A, B, C, M, N, K) on contiguous row-major tensors."""
+    import torch
+    _require_device_f32(A, "A")
+    _require_device_f32(B, "B")
+    M, K = A.shape
+    N = B.shape[1]
+    if C is None:
+        C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    op_quantized_mm(A, B, C, DEFAULT_RANGE)
+    return C
+
+
+# ------------------------------------------------------------------------- packed operands
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class Packed:
+    """A packed (quantized, MFMA-ready) operand: [scale f32][reserved u32][q int8, rows_pad x k_pad]."""
+
+    def __init__(self, buf, rows: int, k: int, range_: float):
+        self.buf, self.rows, self.k, self.range = buf, rows, k, range_
+        self.rows_pad, self.k_pad = _round_up(rows, ROW_PAD), _round_up(k, K_PAD)
+
+    @property
+    def scale(self):
+        """Cx (for A) or Cw (for B), padded to rows_pad."""
+        import torch
+        return self.buf[: 4 * self.rows_pad].view(torch.float32)
+
+    @property
+    def q(self):
+        """X_int8 (rows_pad x k_pad) or W_int8^T (n_pad x k_pad), zero padded."""
+        import torch
+        off = 8 * self.rows_pad
+        return self.buf[off: off + self.rows_pad * self.k_pad].view(torch.int8).view(self.rows_pad, self.k_pad)
+
+
+def _alloc_packed(rows, k, device):
+    import torch
+    nbytes = load().qgemm_packed_size(rows, k)
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def pack_a(A, range: float = DEFAULT_RANGE) -> Packed:  # noqa: A002
+    """Cx = absmax rows (op_mm.cuh:76-77) and X_int8 (op_mm.cuh:82-87), fused."""
+    _require_device_f32(A, "A")
+    M, K = A.shape
+    p = Packed(_alloc_packed(M, K, A.device), M, K, range)
+    _check("qgemm_pack_a", load().qgemm_pack_a(A.data_ptr(), A.stride(0), A.stride(1), M, K, float(range),
+                                              p.buf.data_ptr(), _stream(A.device)))
+    return p
+
+
+def pack_b(B, range: float = DEFAULT_RANGE) -> Packed:  # noqa: A002
+    """Cw = absmax columns (op_mm.cuh:78-79) and W_int8 (op_mm.cuh:84-89), stored transposed."""
+    _require_device_f32(B, "B")
+    K, N = B.shape
+    p = Packed(_alloc_packed(N, K, B.device), N, K, range)
+    _check("qgemm_pack_b", load().qgemm_pack_b(B.data_ptr(), B.stride(0), B.stride(1), K, N, float(range),
+                                              p.buf.data_ptr(), _stream(B.device)))
+    return p
+
+
+def mm_packed(pa: Packed, pb: Packed, C=None):
+    """int8 MFMA GEMM + fused dequantize (op_mm.cuh:92-99) on packed operands."""
+    import torch
+    assert pa.k == pb.k, "X.w == W.h"
+    if C is None:
+        C = torch.empty((pa.rows, pb.rows), dtype=torch.float32, device=pa.buf.device)
+    _require_device_f32(C, "C")
+    assert C.shape == (pa.rows, pb.rows)
+    _check("qgemm_mm_packed", load().qgemm_mm_packed(pa.buf.data_ptr(), pb.buf.data_ptr(), C.data_ptr(), C.stride(0),
+                                                    C.stride(1), pa.rows, pb.rows, pa.k, float(pa.range),
+                                                    _stream(C.device)))
+    return C
+
+
+def mm_packed_i32(pa: Packed, pb: Packed):
+    """The raw int32 accumulator O_int32 (op_mm.cuh:92-93)."""
+    import torch
+    acc = torch.empty((pa.rows, pb.rows), dtype=torch.int32, device=pa.buf.device)
+    _check("qgemm_mm_packed_i32", load().qgemm_mm_packed_i32(pa.buf.data_ptr(), pb.buf.data_ptr(), acc.data_ptr(),
+                                                            pa.rows, pb.rows, pa.k, _stream(acc.device)))
+    return acc
+
+
+def mm_fp32(A, B, C=None):
+    """The reference's unquantized op_mm<float,float> (op_mm.cuh:49-65), bit-exact, on the GPU."""
+    import torch
+    _require_device_f32(A, "A")
+    _require_device_f32(B, "B")
+    M, K = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == K
+    if C is None:
+        C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    _check("qgemm_mm_fp32", load().qgemm_mm_fp32(A.data_ptr(), A.stride(0), A.stride(1), B.data_ptr(), B.stride(0),
+                                                B.stride(1), C.data_ptr(), C.stride(0), C.stride(1), M, N, K,
+                                                _stream(A.device)))
+    return C
+
+
+def fill_uniform(t, seed: int, lo: float = -1.0, hi: float = 1.0):
+    """Seeded U[lo,hi) fill of a contiguous fp32 device tensor (bit-identical to the oracle's)."""
+    assert t.is_contiguous()
+    _check("qgemm_fill_uniform", load().qgemm_fill_uniform(t.data_ptr(), t.numel(), seed, lo, hi, _stream(t.device)))
+    return t
+
+
+from . import shard  # noqa: E402,F401  (M-sharding helpers; pure Python)

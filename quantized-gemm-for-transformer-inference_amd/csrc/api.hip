@@ -1,0 +1,171 @@
+// api.hip -- the C-ABI of include/qgemm.h: argument checks, layout dispatch, workspace, stream order.
+//
+// op_quantized_mm (/root/reference/src/ops/op_mm.cuh:67-101) runs ten launches and allocates eight
+// temporaries per call.  Here a call is three stream-ordered launch groups on caller memory plus a
+// grow-only cached workspace:
+//   pack A  (Cx + X_int8)          -- op_mm.cuh:76-77, 82-83, 86-87
+//   pack B  (Cw + W_int8^T)        -- op_mm.cuh:78-79, 84-85, 88-89
+//   MFMA GEMM + dequant epilogue   -- op_mm.cuh:92-99
+#include <mutex>
+#include <stdio.h>
+
+#include "../../include/qgemm.h"
+#include "qgemm_internal.h"
+
+using namespace qgemm;
+
+namespace {
+
+constexpr float kDefaultRange = 127.0f;  // `range` at every reference call site (test_quantize.cu:76)
+
+int err(hipError_t e) { return (int)e; }
+
+bool dims_ok(int m, int n, int k) { return m >= 0 && n >= 0 && k >= 1; }
+
+// Which packing pass serves a matrix whose reduction vectors are its rows (row_stride, elem_stride)?
+//   elem_stride == 1       : the vectors are contiguous        -> pack_rows (vector path)
+//   row_stride  == 1       : the vectors are columns of a row-major image -> pack_cols
+//   anything else          : pack_rows generic (scalar, strided)
+hipError_t pack_vectors(const float *src, int64_t row_stride, int64_t elem_stride, int rows, int len, float range,
+                        PackedView out, hipStream_t stream) {
+    if (elem_stride == 1) return launch_pack_rows(src, row_stride, 1, rows, len, range, out, stream);
+    if (row_stride == 1 && len > 1) return launch_pack_cols(src, elem_stride, len, rows, range, out, stream);
+    return launch_pack_rows(src, row_stride, elem_stride, rows, len, range, out, stream);
+}
+
+// Grow-only workspace per device, for the entry points without an explicit workspace.
+struct CachedWs {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_ws_mu;
+CachedWs g_ws[64];
+
+hipError_t cached_workspace(size_t need, void **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    CachedWs &w = g_ws[dev];
+    if (w.bytes < need) {
+        if (w.ptr) {
+            // a previous call may still be using it on some stream
+            if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+            if ((e = hipFree(w.ptr)) != hipSuccess) return e;
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        size_t grow = need + need / 8;  // headroom for nearby shapes
+        if ((e = hipMalloc(&w.ptr, grow)) != hipSuccess) return e;
+        w.bytes = grow;
+    }
+    *out = w.ptr;
+    return hipSuccess;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+size_t qgemm_packed_size(int rows, int k) {
+    if (rows < 0 || k < 1) return 0;
+    return packed_bytes(rows, k);
+}
+
+size_t op_mm_quantize_workspace_size(int m, int n, int k) {
+    if (!dims_ok(m, n, k)) return 0;
+    return align256(packed_bytes(m, k)) + align256(packed_bytes(n, k));
+}
+
+int qgemm_pack_a(const float *A, int64_t a_stride_h, int64_t a_stride_w, int m, int k, float range, void *packed_a,
+                 void *stream) {
+    if (!A || !packed_a || m < 0 || k < 1) return err(hipErrorInvalidValue);
+    if (m == 0) return 0;
+    // reduction vectors = rows of A: (row stride, element stride) = (stride_h, stride_w)
+    return err(pack_vectors(A, a_stride_h, a_stride_w, m, k, range, packed_view(packed_a, m, k),
+                            static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_pack_b(const float *B, int64_t b_stride_h, int64_t b_stride_w, int k, int n, float range, void *packed_b,
+                 void *stream) {
+    if (!B || !packed_b || n < 0 || k < 1) return err(hipErrorInvalidValue);
+    if (n == 0) return 0;
+    // reduction vectors = columns of B: (vector stride, element stride) = (stride_w, stride_h)
+    return err(pack_vectors(B, b_stride_w, b_stride_h, n, k, range, packed_view(packed_b, n, k),
+                            static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_mm_packed(const void *packed_a, const void *packed_b, float *C, int64_t c_stride_h, int64_t c_stride_w,
+                    int m, int n, int k, float range, void *stream) {
+    if (!packed_a || !packed_b || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    const float inv_r2 = 1.0f / (range * range);  // op_mm.cuh:99, one rounding per operation (host IEEE)
+    return err(launch_gemm_dequant(packed_view(packed_a, m, k), packed_view(packed_b, n, k), C, c_stride_h,
+                                   c_stride_w, m, n, inv_r2, static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_mm_packed_i32(const void *packed_a, const void *packed_b, int32_t *Acc, int m, int n, int k, void *stream) {
+    if (!packed_a || !packed_b || !Acc || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    return err(launch_gemm_i32(packed_view(packed_a, m, k), packed_view(packed_b, n, k), Acc, m, n,
+                               static_cast<hipStream_t>(stream)));
+}
+
+int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, const float *B, int64_t b_stride_h,
+                      int64_t b_stride_w, float *C, int64_t c_stride_h, int64_t c_stride_w, int m, int n, int k,
+                      float range, void *workspace, size_t ws_bytes, void *stream) {
+    // op_mm.cuh:71-72: shape agreement and device residency are asserted by the reference
+    if (!A || !B || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    const size_t need = op_mm_quantize_workspace_size(m, n, k);
+    if (!workspace || ws_bytes < need) return err(hipErrorInvalidValue);
+    char *pa = static_cast<char *>(workspace);
+    char *pb = pa + align256(packed_bytes(m, k));
+    int rc = qgemm_pack_a(A, a_stride_h, a_stride_w, m, k, range, pa, stream);
+    if (rc) return rc;
+    rc = qgemm_pack_b(B, b_stride_h, b_stride_w, k, n, range, pb, stream);
+    if (rc) return rc;
+    return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);
+}
+
+int op_mm_quantize_ex(const float *A, int64_t a_stride_h, int64_t a_stride_w, const float *B, int64_t b_stride_h,
+                      int64_t b_stride_w, float *C, int64_t c_stride_h, int64_t c_stride_w, int m, int n, int k,
+                      float range, void *stream) {
+    if (!A || !B || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    const size_t need = op_mm_quantize_workspace_size(m, n, k);
+    void *ws = nullptr;
+    hipError_t e = cached_workspace(need, &ws);
+    if (e != hipSuccess) return err(e);
+    return op_mm_quantize_ws(A, a_stride_h, a_stride_w, B, b_stride_h, b_stride_w, C, c_stride_h, c_stride_w, m, n, k,
+                             range, ws, need, stream);
+}
+
+int op_mm_quantize(const float *A, const float *B, float *C, int m, int n, int k) {
+    return op_mm_quantize_ex(A, k, 1, B, n, 1, C, n, 1, m, n, k, kDefaultRange, nullptr);
+}
+
+int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride_w, const float *B, int64_t b_stride_h,
+                  int64_t b_stride_w, float *C, int64_t c_stride_h, int64_t c_stride_w, int m, int n, int k,
+                  void *stream) {
+    if (!A || !B || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    return err(launch_mm_f32(A, a_stride_h, a_stride_w, B, b_stride_h, b_stride_w, C, c_stride_h, c_stride_w, m, n, k,
+                             static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, void *stream) {
+    if (!dst || count < 0) return err(hipErrorInvalidValue);
+    return err(launch_fill_uniform(dst, count, seed, lo, hi, static_cast<hipStream_t>(stream)));
+}
+
+const char *qgemm_version(void) {
+    static char buf[160];
+    snprintf(buf, sizeof buf, "qgemm 0.1.0 gfx950 %s", gemm_config_name());
+    return buf;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// qgemm_internal.h -- shared definitions of the gfx950 quantized-GEMM kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qgemm {
+
+// Packed operand geometry (include/qgemm.h): rows padded to the GEMM macro-tile, k to its k-step.
+constexpr int kRowPad = 256;
+constexpr int kKPad = 128;
+
+__host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// Layout of one packed operand buffer: [scale: rows_pad f32][scratch: rows_pad u32][q: rows_pad x k_pad i8].
+// The scratch words hold the column-absmax partials of pack_cols (pass 1 -> pass 2).
+struct PackedView {
+    float *scale;       // rows_pad floats (Cx or Cw)
+    uint32_t *scratch;  // rows_pad words
+    int8_t *q;          // rows_pad x k_pad
+    int64_t rows_pad, k_pad;
+};
+
+inline PackedView packed_view(const void *base, int rows, int k) {
+    PackedView v;
+    v.rows_pad = round_up(rows, kRowPad);
+    v.k_pad = round_up(k, kKPad);
+    char *p = static_cast<char *>(const_cast<void *>(base));
+    v.scale = reinterpret_cast<float *>(p);
+    v.scratch = reinterpret_cast<uint32_t *>(p + v.rows_pad * 4);
+    v.q = reinterpret_cast<int8_t *>(p + v.rows_pad * 8);
+    return v;
+}
+
+inline size_t packed_bytes(int rows, int k) {
+    return (size_t)round_up(rows, kRowPad) * 8 + (size_t)round_up(rows, kRowPad) * round_up(k, kKPad);
+}
+
+// ---- the reference's per-element arithmetic, pinned to single IEEE operations ----------------
+
+// AbsMaxFunc (op_reduction.cuh:11-24) on an element that is not the seed: |x|, skipping NaN.
+// Returned as a candidate for a running maximum started at -inf; the caller combines candidates
+// with strict ">" so NaN never enters.
+__device__ __forceinline__ float absmax_candidate(float x) { return fabsf(x); }
+
+// Final combine with the signed seed (the reduction kernels' first element, op_reduction.cuh:80/105):
+// acc = seed; if (p > acc) acc = p.  A NaN seed sticks, exactly as in the sequential functor.
+__device__ __forceinline__ float absmax_finish(float seed, float p) { return (p > seed) ? p : seed; }
+
+// InvDivideConstFunc (op_elemwise.cuh:131-143): correctly rounded range / C.
+__device__ __forceinline__ float inv_divide(float range, float c) { return __fdiv_rn(range, c); }
+
+// MultiplyWithTypecastFunc<float,int8_t> (op_elemwise.cuh:106-114): static_cast<int8_t>(x*s),
+// truncation toward zero; saturation and NaN->0 where C++ leaves the cast undefined.
+__device__ __forceinline__ int quant_i8(float x, float s) {
+    float v = __fmul_rn(x, s);
+    v = (v != v) ? 0.0f : v;
+    v = fminf(fmaxf(v, -128.0f), 127.0f);
+    return (int)v;  // in range: v_cvt_i32_f32 truncates
+}
+
+// op_mm(Cx, Cw) with K = 1 (op_mm.cuh:96-97): res = 0; res += Cx*Cw -> fl(Cx*Cw) + 0 (turns -0 into +0).
+__device__ __forceinline__ float outer_product(float cx, float cw) { return __fadd_rn(__fmul_rn(cx, cw), 0.0f); }
+
+// op_dequantize (DequantizeFunc, op_elemwise.cuh:93-103) then op_multiply(O, 1/(range*range))
+// (op_mm.cuh:99): two separate launches in the reference, so two roundings, no contraction.
+__device__ __forceinline__ float dequantize(int acc, float outer, float inv_r2) {
+    return __fmul_rn(__fmul_rn((float)acc, outer), inv_r2);
+}
+
+// Counter-based generator shared with oracle_uniform_at (oracle/qgemm_oracle.c).
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// ---- launchers (defined in the .hip files) ------------------------------------------------------
+hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, int len, float range,
+                            PackedView out, hipStream_t stream);
+hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
+                            hipStream_t stream);
+hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
+hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
+                               int m, int n, float inv_r2, hipStream_t stream);
+hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
+                           hipStream_t stream);
+hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
+                         int64_t csh, int64_t csw, int m, int n, int k, hipStream_t stream);
+const char *gemm_config_name();
+
+}  // namespace qgemm

@@ -1,0 +1,95 @@
+"""The C-ABI library: builds for gfx950, loads, exports exactly what include/qgemm.h declares,
+and rejects bad arguments (the reference's asserts, op_mm.cuh:71-72) without touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "qgemm.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    return sorted(re.findall(r"^QGEMM_API\s+[\w\s\*]+?\b((?:op_|qgemm_)\w+)\s*\(", text, flags=re.M))
+
+
+def exported(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], check=True, capture_output=True, text=True).stdout
+    return sorted(line.split()[-1] for line in out.splitlines() if " T " in line)
+
+
+def test_header_declares_the_north_star_entry_point():
+    fns = header_functions()
+    assert "op_mm_quantize" in fns
+    # op_mm_quantize(A, B, C, M, N, K): three pointers and three ints, no parameter named N
+    text = open(HEADER).read()
+    assert re.search(r"int op_mm_quantize\(const float \*A, const float \*B, float \*C, int m, int n, int k\);", text)
+    assert not re.search(r"\bint N\b", text), "the reference #defines N (op_elemwise.cuh:10)"
+
+
+def test_library_exports_every_declared_symbol(qg):
+    assert header_functions() == sorted(qg.EXPORTED_SYMBOLS)
+    assert exported(qg.LIB_PATH) == header_functions(), "exports must be exactly the C-ABI"
+
+
+def test_library_carries_gfx950_code_object(qg):
+    blob = open(qg.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_version_and_sizes_without_gpu(qg):
+    L = qg.load()
+    assert "gfx950" in qg.version()
+    # packed operand: [scale rows_pad*4][reserved rows_pad*4][rows_pad*k_pad]
+    assert L.qgemm_packed_size(4096, 4096) == 4096 * 8 + 4096 * 4096
+    assert L.qgemm_packed_size(1, 1) == 256 * 8 + 256 * 128
+    assert L.qgemm_packed_size(257, 129) == 512 * 8 + 512 * 256
+    ws = L.op_mm_quantize_workspace_size(4096, 4096, 4096)
+    assert ws == 2 * (4096 * 8 + 4096 * 4096)
+    assert L.op_mm_quantize_workspace_size(4, 4, 0) == 0
+
+
+@pytest.mark.parametrize("args", [
+    (None, None, None, 4, 4, 4),
+    (8, 8, 8, 4, 4, 0),      # K = 0: no reduction vector
+    (8, 8, 8, -1, 4, 4),
+])
+def test_invalid_arguments_return_hip_error_invalid_value(qg, args):
+    L = qg.load()
+    a, b, c, m, n, k = args
+    assert L.op_mm_quantize(a, b, c, m, n, k) == qg.HIP_ERROR_INVALID_VALUE
+
+
+def test_invalid_pack_and_workspace_calls(qg):
+    L = qg.load()
+    assert L.qgemm_pack_a(None, 4, 1, 4, 4, 127.0, 8, None) == 1
+    assert L.qgemm_pack_b(8, 4, 1, 0, 4, 127.0, 8, None) == 1
+    # too small an explicit workspace is refused before any launch
+    assert L.op_mm_quantize_ws(8, 4, 1, 8, 4, 1, 8, 4, 1, 4, 4, 4, 127.0, 8, 16, None) == 1
+    assert L.qgemm_mm_packed(None, 8, 8, 4, 1, 4, 4, 4, 127.0, None) == 1
+
+
+def test_harness_binaries_built(qg):
+    for exe in ("test_quantize", "timing_quantize"):
+        p = os.path.join(qg.PKG_DIR, "build", exe)
+        assert os.access(p, os.X_OK), p
+
+
+def test_missing_library_fails_loudly(qg, monkeypatch, tmp_path):
+    """No CPU fallback: without the HIP library every entry point raises."""
+    monkeypatch.setattr(qg, "LIB_PATH", str(tmp_path / "libqgemm.so"))
+    monkeypatch.setattr(qg, "_lib", None)
+    with pytest.raises(RuntimeError, match="not built"):
+        qg.load()
+
+
+def test_reference_side_ctypes_binding_matches(qg):
+    """The ctypes stub shown in INTEGRATION.md binds the same signature."""
+    L = ctypes.CDLL(qg.LIB_PATH)
+    f = L.op_mm_quantize
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3
+    f.restype = ctypes.c_int
+    assert f(None, None, None, 1, 1, 1) == 1

@@ -1,0 +1,183 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle, bit for bit.
+
+Every test here runs the product path -- libqgemm.so's gfx950 kernels -- and compares with the
+oracle (tests only) or the committed fixtures.  Bar: O, Xq, Wq, Acc bit-identical; scales Cx/Cw
+value-identical (their zero sign never reaches O: fl(Cx*Cw)+0 is +0 either way).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from util import assert_bits_equal, assert_values_equal, load_cases, load_kat
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, device):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def _run_full(qg, X, W, device):
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    O = torch.full((X.shape[0], W.shape[1]), float("nan"), device=device)  # poisoned
+    qg.op_quantized_mm(Xd, Wd, O, 127.0)
+    torch.cuda.synchronize()
+    return O.cpu().numpy()
+
+
+def _check_intermediates(qg, X, W, ref, device, name):
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    pa, pb = qg.pack_a(Xd), qg.pack_b(Wd)
+    M, K = X.shape
+    N = W.shape[1]
+    torch.cuda.synchronize()
+    assert_values_equal(pa.scale[:M].cpu().numpy(), ref["Cx"], f"{name} Cx")
+    assert_values_equal(pb.scale[:N].cpu().numpy(), ref["Cw"], f"{name} Cw")
+    qa, qb = pa.q.cpu().numpy(), pb.q.cpu().numpy()
+    assert (qa[:M, :K] == ref["Xq"]).all(), f"{name} Xq"
+    assert (qb[:N, :K] == ref["Wq"].T).all(), f"{name} Wq"
+    assert not qa[M:].any() and not qa[:, K:].any(), f"{name} A padding not zero"
+    assert not qb[N:].any() and not qb[:, K:].any(), f"{name} B padding not zero"
+    acc = qg.mm_packed_i32(pa, pb).cpu().numpy()
+    assert (acc == ref["Acc"]).all(), f"{name} Acc"
+
+
+def test_kat1_reference_fixture(qg, device):
+    k = load_kat()["kat1"]
+    X, W = np.array(k["X"], np.float32), np.array(k["W"], np.float32)
+    want = np.array([int(b, 16) for b in k["O_bits"]], np.uint32).view(np.float32).reshape(3, 2)
+    assert_bits_equal(_run_full(qg, X, W, device), want, "KAT-1")
+    C = qg.mm_fp32(_dev(X, device), _dev(W, device)).cpu().numpy()
+    assert C.tolist() == k["unquantized"]
+
+
+def test_explicit_edge_fixtures(qg, device):
+    """Quirk (with/without int8 overflow), zero rows/cols, NaN/inf, K=1, M=1, N=1, extremes."""
+    index, arrays = load_cases()
+    for rec in index:
+        if rec["kind"] != "explicit":
+            continue
+        n = rec["name"]
+        X, W = arrays[n + "/X"], arrays[n + "/W"]
+        assert_bits_equal(_run_full(qg, X, W, device), arrays[n + "/O"], n)
+        ref = {key: arrays[f"{n}/{key}"] for key in ("Cx", "Cw", "Xq", "Wq", "Acc")}
+        _check_intermediates(qg, X, W, ref, device, n)
+
+
+def test_seeded_fixtures(qg, oracle, device):
+    index, _ = load_cases()
+    for rec in index:
+        if rec["kind"] != "seeded":
+            continue
+        X, W = oracle.inputs(rec["M"], rec["N"], rec["K"], rec["seed"])
+        O, ref = oracle.quantized_mm(X, W, intermediates=True)
+        assert_bits_equal(_run_full(qg, X, W, device), O, rec["name"])
+        _check_intermediates(qg, X, W, ref, device, rec["name"])
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 384), (1000, 300, 1030), (64, 4096, 256), (2048, 2048, 2048)])
+def test_random_shapes_full_oracle(qg, oracle, device, M, N, K):
+    X, W = oracle.inputs(M, N, K, 21)
+    assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
+
+
+def test_device_generator_matches_oracle(qg, oracle, device):
+    t = torch.empty(1 << 20, device=device)
+    qg.fill_uniform(t, seed=9)
+    assert_bits_equal(t.cpu().numpy(), oracle.uniform((1 << 20,), seed=9), "fill_uniform")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (2048, 16384, 4096), (2048, 4096, 16384)])
+def test_full_size_sampled_rows(qg, oracle, device, M, N, K):
+    """BASELINE configs 2 and 3 at full size: inputs generated on the GPU (bit-identical to the
+    oracle's generator), output rows sampled across every macro-tile row and checked bit-exactly."""
+    X = qg.fill_uniform(torch.empty((M, K), device=device), seed=2 * 31)
+    W = qg.fill_uniform(torch.empty((K, N), device=device), seed=2 * 31 + 1)
+    O = qg.op_mm_quantize(X, W)
+    torch.cuda.synchronize()
+    Xh, Wh = oracle.uniform((M, K), 2 * 31), oracle.uniform((K, N), 2 * 31 + 1)
+    assert_bits_equal(X.cpu().numpy()[:3], Xh[:3], "X generation")
+    rows = np.unique(np.concatenate([np.arange(0, M, 257), [M - 1, 255, 256, M // 2]])).astype(np.int32)
+    want = oracle.quantized_mm_rows(Xh, Wh, rows)
+    assert_bits_equal(O[torch.from_numpy(rows).long().to(device)].cpu().numpy(), want, f"{M}x{N}x{K} rows")
+
+
+def test_strided_views(qg, oracle, device):
+    """Transposed and sliced views, as the reference's Index() macro allows (tensor.cuh:121-149)."""
+    M, N, K = 200, 150, 260
+    X, W = oracle.inputs(M, N, K, 33)
+    want = oracle.quantized_mm(X, W)
+    Xt = _dev(np.ascontiguousarray(X.T), device).T      # X column-major  -> pack_cols path for A
+    Wt = _dev(np.ascontiguousarray(W.T), device).T      # W column-major  -> pack_rows path for B
+    big = torch.full((M + 7, N + 9), float("nan"), device=device)
+    O = big[3:3 + M, 5:5 + N]                           # strided output
+    qg.op_quantized_mm(Xt, Wt, O, 127.0)
+    torch.cuda.synchronize()
+    assert_bits_equal(O.cpu().numpy(), want, "transposed operands, sliced output")
+    assert torch.isnan(big[:3]).all() and torch.isnan(big[:, :5]).all(), "wrote outside the view"
+    # fully generic strides (every other column of a wider buffer)
+    Xw = _dev(np.repeat(X, 2, axis=1), device)[:, ::2]
+    Ww = _dev(np.repeat(W, 2, axis=0), device)[::2]
+    O2 = torch.empty((M, N), device=device).T.contiguous().T  # column-major output
+    qg.op_quantized_mm(Xw, Ww, O2, 127.0)
+    torch.cuda.synchronize()
+    assert_bits_equal(O2.cpu().numpy(), want, "generic strides, column-major output")
+
+
+def test_c_abi_null_stream_entry_point(qg, oracle, device):
+    """The flat op_mm_quantize(A,B,C,M,N,K) on the null stream, as a C caller would use it."""
+    M, N, K = 300, 257, 129
+    X, W = oracle.inputs(M, N, K, 41)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    O = torch.empty((M, N), device=device)
+    torch.cuda.synchronize()
+    rc = qg.load().op_mm_quantize(Xd.data_ptr(), Wd.data_ptr(), O.data_ptr(), M, N, K)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert_bits_equal(O.cpu().numpy(), oracle.quantized_mm(X, W), "op_mm_quantize")
+
+
+def test_explicit_workspace_and_prepacked_weights(qg, oracle, device):
+    M, N, K = 384, 512, 640
+    X, W = oracle.inputs(M, N, K, 51)
+    want = oracle.quantized_mm(X, W)
+    L = qg.load()
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    ws = torch.empty(L.op_mm_quantize_workspace_size(M, N, K), dtype=torch.uint8, device=device)
+    O = torch.empty((M, N), device=device)
+    s = qg._stream(device)
+    rc = L.op_mm_quantize_ws(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, 127.0,
+                             ws.data_ptr(), ws.numel(), s)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert_bits_equal(O.cpu().numpy(), want, "explicit workspace")
+    pb = qg.pack_b(Wd)  # weight packed once, reused
+    for _ in range(2):
+        O2 = qg.mm_packed(qg.pack_a(Xd), pb)
+        torch.cuda.synchronize()
+        assert_bits_equal(O2.cpu().numpy(), want, "prepacked B")
+
+
+def test_unquantized_gemm_matches_reference_order(qg, oracle, device):
+    """qgemm_mm_fp32 is the reference's op_mm<float,float>: sequential-k fmaf, bit-exact."""
+    for M, N, K in [(100, 70, 96), (33, 65, 130)]:
+        X, W = oracle.inputs(M, N, K, 61)
+        C = qg.mm_fp32(_dev(X, device), _dev(W, device)).cpu().numpy()
+        assert_bits_equal(C, oracle.mm_fp32(X, W), f"fp32 {M}x{N}x{K}")
+
+
+def test_harness_binary_reproduces_reference_output(qg):
+    import os
+    import subprocess
+    exe = os.path.join(qg.PKG_DIR, "build", "test_quantize")
+    out = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=120).stdout
+    lines = [ln.strip() for ln in out.splitlines()]
+    q = lines.index("Quantized result:")
+    assert lines[q + 1].split() == ["-1.007874", "0.000000"]
+    assert lines[q + 2].split() == ["-1.984252", "-2.031496"]
+    assert lines[q + 3].split() == ["1.000000", "2.000000"]
+    e = lines.index("Mean quantization error:")
+    assert abs(float(lines[e + 1]) - 0.003937006) < 1e-8
+    assert "All tests completed successfully!" in lines
