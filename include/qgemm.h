@@ -64,7 +64,8 @@ QGEMM_API int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_st
 
 /* ---- The chain's stages (the reference's L2 primitives, fused MI355X-style) ----------------
  * Packed operand = the quantized operand in MFMA-ready form, in ONE device buffer:
- *   [ scale: rows_pad f32 ][ reserved: rows_pad u32 ][ q: rows_pad x k_pad int8, row-major, zero padded ]
+ *   [ scale: rows_pad f32 ][ reserved: parts x rows_pad u32, padded to 256 B ][ q: rows_pad x k_pad int8,
+ *     row-major, zero padded ]   with parts = max(1, ceil((k-1)/256))
  * rows_pad = round_up(rows, 256), k_pad = round_up(k, 128).  For A, rows = m and the scale is
  * Cx (op_absmax(X,Cx), op_mm.cuh:76-77) and q = X_int8 (op_mm.cuh:86-87).  For B, rows = n
  * (B is stored transposed, k contiguous) and the scale is Cw (op_mm.cuh:78-79), q = W_int8^T.
@@ -91,6 +92,11 @@ QGEMM_API int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride
 /* Deterministic U[lo,hi) fill, bit-identical to oracle_fill_uniform (stands in for the
  * reference's cuRAND op_uniform_init, op_elemwise.cuh:728-744). */
 QGEMM_API int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, void *stream);
+
+/* Diagnostics: record hipEvent_t start_event / stop_event exactly at the start and end of the GEMM
+ * kernel of the NEXT op_mm_quantize* / qgemm_mm_packed call made by this thread (then cleared).
+ * Used by bench.py to time the dominant kernel inside its timed region.  NULL, NULL = off. */
+QGEMM_API int qgemm_set_gemm_events(void *start_event, void *stop_event);
 
 /* Library identification: "qgemm <version> gfx950 <kernel config>". */
 QGEMM_API const char *qgemm_version(void);

@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "qgemm_mm_packed",
     "qgemm_mm_packed_i32",
     "qgemm_mm_fp32",
+    "qgemm_set_gemm_events",
     "qgemm_fill_uniform",
     "qgemm_version",
 )
@@ -104,6 +105,8 @@ def load() -> ctypes.CDLL:
         L.qgemm_mm_fp32.restype = i32
         L.qgemm_fill_uniform.argtypes = [vp, i64, ctypes.c_uint64, f32, f32, vp]
         L.qgemm_fill_uniform.restype = i32
+        L.qgemm_set_gemm_events.argtypes = [vp, vp]
+        L.qgemm_set_gemm_events.restype = i32
         L.qgemm_version.argtypes = []
         L.qgemm_version.restype = ctypes.c_char_p
         _lib = L
@@ -171,7 +174,7 @@ def _round_up(x: int, m: int) -> int:
 
 
 class Packed:
-    """A packed (quantized, MFMA-ready) operand: [scale f32][reserved u32][q int8, rows_pad x k_pad]."""
+    """A packed (quantized, MFMA-ready) operand: [scale f32][reserved u32 partials][q int8, rows_pad x k_pad]."""
 
     def __init__(self, buf, rows: int, k: int, range_: float):
         self.buf, self.rows, self.k, self.range = buf, rows, k, range_
@@ -187,7 +190,8 @@ class Packed:
     def q(self):
         """X_int8 (rows_pad x k_pad) or W_int8^T (n_pad x k_pad), zero padded."""
         import torch
-        off = 8 * self.rows_pad
+        parts = -(-(self.k - 1) // 256) if self.k > 1 else 1
+        off = _round_up(4 * self.rows_pad * (1 + parts), 256)
         return self.buf[off: off + self.rows_pad * self.k_pad].view(torch.int8).view(self.rows_pad, self.k_pad)
 
 

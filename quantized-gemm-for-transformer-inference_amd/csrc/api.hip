@@ -124,6 +124,18 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     if (!workspace || ws_bytes < need) return err(hipErrorInvalidValue);
     char *pa = static_cast<char *>(workspace);
     char *pb = pa + align256(packed_bytes(m, k));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // Common case (row-major X and W): X's row pass and W's column-absmax pass share one launch,
+    // then W's quantize/transpose pass, then the GEMM -- three launches in all.
+    if (a_stride_w == 1 && b_stride_w == 1 && k > 1) {
+        const PackedView va = packed_view(pa, m, k), vb = packed_view(pb, n, k);
+        hipError_t e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
+        if (e == hipSuccess) {
+            if ((e = launch_pack_cols_pass2(B, b_stride_h, k, n, range, vb, s)) != hipSuccess) return err(e);
+            return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);
+        }
+        if (e != hipErrorNotSupported) return err(e);
+    }
     int rc = qgemm_pack_a(A, a_stride_h, a_stride_w, m, k, range, pa, stream);
     if (rc) return rc;
     rc = qgemm_pack_b(B, b_stride_h, b_stride_w, k, n, range, pb, stream);
@@ -155,6 +167,11 @@ int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride_w, const 
     if (m == 0 || n == 0) return 0;
     return err(launch_mm_f32(A, a_stride_h, a_stride_w, B, b_stride_h, b_stride_w, C, c_stride_h, c_stride_w, m, n, k,
                              static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_set_gemm_events(void *start_event, void *stop_event) {
+    set_gemm_events(static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event));
+    return 0;
 }
 
 int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, void *stream) {

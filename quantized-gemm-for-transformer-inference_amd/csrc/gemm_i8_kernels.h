@@ -1,0 +1,415 @@
+// gemm_i8_kernels.h -- the int8 MFMA GEMM kernels (included by gemm_i8.hip and by the lab harness).
+//
+// C[i,j] = dequant(sum_k A[i,k] * B[j,k]) with A = Xq [m_pad][k_pad], B = Wq^T [n_pad][k_pad] (packed,
+// k-contiguous, zero padded).  Macro-tile 256 x 256, k-step 128 bytes, 512 threads = 8 waves as
+// 2 (M) x 4 (N), each wave 128 x 64 = 4 x 2 tiles of v_mfma_i32_32x32x32_i8.
+//
+// Staging: global_load_lds_dwordx4 (1 KiB per wave instruction = 8 rows x 128 B) into a 2-deep LDS
+// ring of 64 KiB stages; chunk g of LDS row r sits at slot g ^ ((r>>1)&7) (swizzle on the SOURCE
+// address; the LDS image stays lane-linear), which makes the fragment reads -- ds_read_b128 of one
+// 16-B chunk from 32 consecutive rows -- bank-conflict free.
+#pragma once
+
+#include "qgemm_internal.h"
+
+namespace qgemm {
+namespace gemm {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 256, BN = 256, BK = 128;
+constexpr int kThreads = 512;
+constexpr int kTileBytes = BM * BK;          // 32 KiB per operand per stage
+constexpr int kStageBytes = 2 * kTileBytes;  // A + B
+constexpr int kLdsBytes = 2 * kStageBytes;   // 2-deep ring = 128 KiB
+
+static_assert(BM == kRowPad && BN == kRowPad && BK == kKPad, "packed layout must match the macro-tile");
+
+// Epilogue variants
+enum StoreMode { kStoreDirect = 0, kStoreLds = 1, kStoreNone = 2 };
+
+// Block -> macro-tile.  Blocks b and b+8 are dispatched to the same XCD; give each XCD a contiguous
+// range of logical ids (bijective for any grid size), then walk logical ids in groups of kGroupM
+// tile-rows so one XCD's range covers a compact patch (shared A and B panels stay in its L2).
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int &tm, int &tn) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    constexpr int kGroupM = 4;
+    const int per_group = kGroupM * tiles_n;
+    const int group = wgid / per_group;
+    const int first_m = group * kGroupM;
+    const int gsz = min(tiles_m - first_m, kGroupM);
+    const int w = wgid - group * per_group;
+    tm = first_m + w % gsz;
+    tn = w / gsz;
+}
+
+struct GemmArgs {
+    const int8_t *A;
+    const int8_t *B;
+    const float *Cx;
+    const float *Cw;
+    void *C;
+    int64_t csh, csw;
+    int m, n;
+    int64_t k_pad;
+    int tiles_m, tiles_n;
+    float inv_r2;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Shared pieces
+struct Stager {
+    const int8_t *Ablk, *Bblk;
+    int64_t src_off[4];
+    int wave;
+    __device__ __forceinline__ void init(const int8_t *A, const int8_t *B, int tm, int tn, int64_t k_pad, int wave_,
+                                         int lane) {
+        wave = wave_;
+        Ablk = A + (int64_t)tm * BM * k_pad;
+        Bblk = B + (int64_t)tn * BN * k_pad;
+        // wave w fills rows [32w, 32w+32) of both tiles, 8 rows per glds; lane l of instruction i writes
+        // LDS bytes [16l, 16l+16) of its 1-KiB piece = row 32w+8i+(l>>3), slot l&7, which must hold
+        // global chunk g = slot ^ ((row>>1)&7).
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = wave * 32 + i * 8 + (lane >> 3);
+            const int g = (lane & 7) ^ ((row >> 1) & 7);
+            src_off[i] = (int64_t)row * k_pad + g * 16;
+        }
+    }
+    __device__ __forceinline__ void stage(int8_t *lds, int kt, int buf) const {
+        int8_t *la = lds + buf * kStageBytes;
+        int8_t *lb = la + kTileBytes;
+        const int8_t *ga = Ablk + (int64_t)kt * BK;
+        const int8_t *gb = Bblk + (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_global_load_lds((const void *)(ga + src_off[i]), (void *)(la + (wave * 32 + i * 8) * BK),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(gb + src_off[i]), (void *)(lb + (wave * 32 + i * 8) * BK),
+                                             16, 0, 0);
+        }
+    }
+};
+
+// Epilogue for accumulators in the natural C/D map of v_mfma_*_32x32*: col = lane&31,
+// row = (r&3) + 8(r>>2) + 4(lane>>5).  acc[mi][ni] covers rows wm*128+mi*32.., cols wn*64+ni*32..
+template <int kMode, bool kDequant>
+__device__ __forceinline__ void epilogue(const GemmArgs &p, int8_t *lds, v16i (&acc)[4][2], int tm, int tn, int wm,
+                                         int wn, int lane, int tid) {
+    const int gi0 = tm * BM, gj0 = tn * BN;
+    const int lrow = lane & 31, khalf = lane >> 5;
+    if constexpr (kMode == kStoreNone) {
+        // keep the accumulators live without storing them (ablation only)
+        int x = 0;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) x ^= acc[mi][ni][r];
+        if (x == 0x7fffffff && p.m < 0) static_cast<int *>(p.C)[tid] = x;
+        return;
+    } else if constexpr (kMode == kStoreDirect) {
+        if constexpr (kDequant) {
+            float *sCx = reinterpret_cast<float *>(lds);
+            float *sCw = sCx + BM;
+            __syncthreads();
+            if (tid < BM) sCx[tid] = p.Cx[gi0 + tid];
+            else sCw[tid - BM] = p.Cw[gj0 + tid - BM];
+            __syncthreads();
+            float *C = static_cast<float *>(p.C);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int jl = wn * 64 + ni * 32 + lrow;
+                const int j = gj0 + jl;
+                const float cw = sCw[jl];
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int il = wm * 128 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+                        const int i = gi0 + il;
+                        const float o = dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2);
+                        if (i < p.m && j < p.n) C[(int64_t)i * p.csh + (int64_t)j * p.csw] = o;
+                    }
+            }
+        } else {
+            int32_t *C = static_cast<int32_t *>(p.C);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int j = gj0 + wn * 64 + ni * 32 + lrow;
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int i = gi0 + wm * 128 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+                        if (i < p.m && j < p.n) C[(int64_t)i * p.csh + (int64_t)j * p.csw] = acc[mi][ni][r];
+                    }
+            }
+        }
+    } else {
+        // kStoreLds: stage one 128-row half of the 256x256 int32 tile in LDS ([128][256] = 128 KiB),
+        // then every thread dequantizes 4 consecutive columns and writes them as one 16-B store:
+        // a wave instruction covers one whole 1-KiB tile row.
+        int32_t *T = reinterpret_cast<int32_t *>(lds);
+        float *C = static_cast<float *>(p.C);
+        const bool vec = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            __syncthreads();
+            if (wm == half) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int il = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;  // 0..127
+                            const int jl = wn * 64 + ni * 32 + lrow;
+                            T[il * BN + jl] = acc[mi][ni][r];
+                        }
+            }
+            __syncthreads();
+            const int c4 = (tid & 63) * 4;  // column within the tile
+            float cw[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cw[e] = p.Cw[gj0 + c4 + e];  // Cw is padded to n_pad
+#pragma unroll 4
+            for (int rr = tid >> 6; rr < 128; rr += kThreads / 64) {
+                const int i = gi0 + half * 128 + rr;
+                if (i >= p.m) continue;
+                const v4i a = *reinterpret_cast<const v4i *>(T + rr * BN + c4);
+                const float cx = p.Cx[i];
+                if constexpr (kDequant) {
+                    float4 o;
+                    o.x = dequantize(a[0], outer_product(cx, cw[0]), p.inv_r2);
+                    o.y = dequantize(a[1], outer_product(cx, cw[1]), p.inv_r2);
+                    o.z = dequantize(a[2], outer_product(cx, cw[2]), p.inv_r2);
+                    o.w = dequantize(a[3], outer_product(cx, cw[3]), p.inv_r2);
+                    const int j = gj0 + c4;
+                    if (vec && j + 3 < p.n) {
+                        *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = o;
+                    } else {
+                        const float ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = ov[e];
+                    }
+                }
+            }
+        }
+    }
+}
+
+enum V2Flags { kPrio = 1, kNoGlds = 2, kNoLdsRead = 4, kNoBarrier = 8, kNoVmWait = 16 };
+
+// ------------------------------------------------------------------------------------------------
+// v1: stage(kt+1) ; compute(kt) with just-in-time fragment reads ; vmcnt(0) ; barrier
+template <int kMode, bool kDequant>
+__global__ __launch_bounds__(kThreads, 2) void gemm_i8_v1(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    int tm, tn;
+    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    Stager st;
+    st.init(p.A, p.B, tm, tn, p.k_pad, wave, lane);
+    const int lrow = lane & 31, khalf = lane >> 5, swz = (lrow >> 1) & 7;
+    const int a_row0 = (wm * 128 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    v16i acc[4][2];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = v16i{};
+    const int nk = (int)(p.k_pad / BK);
+    st.stage(lds, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) st.stage(lds, kt + 1, cur ^ 1);
+        const int8_t *la = lds + cur * kStageBytes;
+        const int8_t *lb = la + kTileBytes;
+#pragma unroll
+        for (int s = 0; s < BK / 32; ++s) {
+            const int off = ((2 * s + khalf) ^ swz) << 4;
+            v4i a[4], b[2];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 32 * BK + off);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 32 * BK + off);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    epilogue<kMode, kDequant>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+}
+
+// Epilogue for 16x16 accumulators acc[8][4] (wave tile 128 x 64 at rows wm*128, cols wn*64):
+// C/D map col = lane&15, row = 4(lane>>4) + r.
+//   kStoreLds    : dequantize into a [128][256] fp32 LDS image one 128-row half at a time; every wave
+//                  instruction then stores one whole 1-KiB tile row (16 B per lane).  Needs the
+//                  128 KiB staging ring + 2 KiB for the scales.
+//   kStoreDirect : one dword per lane per register (4 rows x 64 B per instruction).
+//   kStoreNone   : ablation -- keep the accumulators live, store nothing.
+template <int kMode>
+__device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (&acc)[8][4], int tm, int tn, int wm,
+                                           int wn, int lane, int tid) {
+    const int gi0 = tm * BM, gj0 = tn * BN;
+    const int lrow = lane & 15, kq = lane >> 4;
+    if constexpr (kMode == kStoreNone) {
+        int x = 0;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x ^= acc[mi][ni][r];
+        if (x == 0x7fffffff && p.m < 0) static_cast<int *>(p.C)[tid] = x;
+        return;
+    }
+    float *sCx = reinterpret_cast<float *>(lds + kLdsBytes);
+    float *sCw = sCx + BM;
+    float *C = static_cast<float *>(p.C);
+    __syncthreads();  // every wave is done with the staging ring
+    if (tid < BM) sCx[tid] = p.Cx[gi0 + tid];
+    else sCw[tid - BM] = p.Cw[gj0 + tid - BM];
+    if constexpr (kMode == kStoreDirect) {
+        __syncthreads();
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int jl = wn * 64 + ni * 16 + lrow;
+            const int j = gj0 + jl;
+            const float cw = sCw[jl];
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int il = wm * 128 + mi * 16 + 4 * kq + r;
+                    const int i = gi0 + il;
+                    const float o = dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2);
+                    if (i < p.m && j < p.n) C[(int64_t)i * p.csh + (int64_t)j * p.csw] = o;
+                }
+        }
+    } else {
+        float *T = reinterpret_cast<float *>(lds);  // [128][256] fp32
+        const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
+                          gj0 + BN <= p.n;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            __syncthreads();
+            if (wm == half) {
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const int jl = wn * 64 + ni * 16 + lrow;
+                    const float cw = sCw[jl];
+#pragma unroll
+                    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int il = mi * 16 + 4 * kq + r;
+                            T[il * BN + jl] =
+                                dequantize(acc[mi][ni][r], outer_product(sCx[half * 128 + il], cw), p.inv_r2);
+                        }
+                }
+            }
+            __syncthreads();
+            const int c4 = (tid & 63) * 4;
+#pragma unroll 4
+            for (int rr = tid >> 6; rr < 128; rr += kThreads / 64) {
+                const int i = gi0 + half * 128 + rr;
+                if (i >= p.m) break;
+                const float4 v = *reinterpret_cast<const float4 *>(T + rr * BN + c4);
+                const int j = gj0 + c4;
+                if (full) {
+                    *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = v;
+                } else {
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// v3: as v2 but on v_mfma_i32_16x16x64_i8 (16 x 16 output per MFMA, 64-deep k).  Per wave 128 x 64 =
+// 8 x 4 tiles; per 64-deep sub-step 8 A + 4 B fragment reads (lane l: row l&15, 16 bytes of k-chunk
+// 4s + (l>>4)) and 32 MFMAs.  C/D map: col = lane&15, row = 4(lane>>4) + reg.
+template <int kMode, bool kDequant, int kFlags = 0>
+__global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + 2048];  // + scales for the epilogue
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    int tm, tn;
+    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    Stager st;
+    st.init(p.A, p.B, tm, tn, p.k_pad, wave, lane);
+    const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
+    const int a_row0 = (wm * 128 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    int off[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+
+    v4i acc[8][4];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4i{};
+
+    auto read_frags = [&](v4i (&a)[8], v4i (&b)[4], int buf, int s) {
+        const int8_t *la = lds + buf * kStageBytes;
+        const int8_t *lb = la + kTileBytes;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[s]);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[s]);
+    };
+    auto mfmas = [&](const v4i (&a)[8], const v4i (&b)[4]) {
+        if constexpr (kFlags & kPrio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        if constexpr (kFlags & kPrio) __builtin_amdgcn_s_setprio(0);
+    };
+
+    const int nk = (int)(p.k_pad / BK);
+    v4i a0[8], b0[4], a1[8], b1[4];
+    st.stage(lds, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    read_frags(a0, b0, 0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (!(kFlags & kNoGlds) || kt == 0)
+            if (more) st.stage(lds, kt + 1, cur ^ 1);
+        read_frags(a1, b1, cur, 1);
+        mfmas(a0, b0);
+        if constexpr (!(kFlags & kNoVmWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (!(kFlags & kNoBarrier)) __syncthreads();
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (more) read_frags(a0, b0, cur ^ 1, 0);
+        mfmas(a1, b1);
+    }
+
+    epilogue16<kMode>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+}
+
+
+}  // namespace gemm
+}  // namespace qgemm

@@ -1,20 +1,22 @@
 // pack.hip -- absmax + quantize kernels (the reference's op_absmax / op_inv_divide / op_multiply
-// steps, op_mm.cuh:75-89), fused into two HBM-streaming passes that emit MFMA-ready int8 operands.
+// steps, op_mm.cuh:75-89), fused into HBM-streaming passes that emit MFMA-ready int8 operands.
 //
-// A "packed operand" (include/qgemm.h) is [scale: rows_pad f32][q: rows_pad x k_pad int8], where each
-// packed row is one reduction vector: a row of X (scale Cx) or a column of W (scale Cw, stored
-// transposed so k is contiguous for the MFMA B fragment).  Padding (rows >= rows, k >= len) is zero.
+// A "packed operand" (include/qgemm.h) is [scale][scratch][q]: each packed row is one reduction
+// vector -- a row of X (scale Cx) or a column of W (scale Cw, stored transposed so k is contiguous for
+// the MFMA B fragment).  Padding rows and k >= len are zero.
 //
-//   pack_rows : the reduction vector is contiguous-ish in memory (X row-major, or W column-major).
-//               One wave per vector: absmax over the vector (wave shuffle reduction), then quantize.
+//   pack_rows : the reduction vector is contiguous (X row-major, or W column-major).  One wave per
+//               vector: absmax (wave shuffle reduction), IEEE range/absmax, truncating quantize.
 //               Replaces op_reduction_kernel_colwise (op_reduction.cuh:71-92: one thread per row,
-//               lanes 16 KiB apart) + op_elemwise_unary_kernel(InvDivideConstFunc) +
-//               op_elemwise_binary_w_bcast_kernel(MultiplyWithTypecastFunc) -- 3 launches, 2 reads.
-//   pack_cols : the reduction vector is strided (W row-major: a column).  Pass 1 reduces coalesced
-//               1024-column strips of 64 rows and merges strips with an order-free integer atomicMax;
-//               pass 2 re-reads W (from the Infinity Cache at the sizes that matter), quantizes and
-//               transposes 128x64 tiles through LDS.
-//               Replaces op_reduction_kernel_rowwise (op_reduction.cuh:96-117) + 2 elementwise launches.
+//               lanes 16 KiB apart) + the InvDivideConstFunc and MultiplyWithTypecastFunc launches.
+//   pack_cols : the reduction vector is a column of a row-major matrix (W).  Pass 1 reduces
+//               256-column x 256-row chunks (coalesced 1-KiB row reads) into one partial per
+//               (chunk, column) -- no atomics and nothing to clear per call; pass 2 reduces the
+//               partials, re-reads W (from the Infinity Cache at the sizes that matter), quantizes
+//               and transposes 128 x 64 tiles through LDS.  Replaces op_reduction_kernel_rowwise
+//               (op_reduction.cuh:96-117) + 2 elementwise launches.
+//   pack_rows_and_colmax : pack_rows(A) and pass 1 of pack_cols(B) in ONE launch (block roles), so
+//               the two HBM streams overlap and a launch boundary disappears.
 #include "qgemm_internal.h"
 
 namespace qgemm {
@@ -34,6 +36,11 @@ __device__ __forceinline__ float cand_max(float p, float x) {
     return (a > p) ? a : p;  // NaN never wins: comparison is false
 }
 
+// partial encoding: candidates are >= +0 and NaN-free, so uint order of (bits + 1) is float order;
+// 0 means "no candidate in this chunk"
+__device__ __forceinline__ uint32_t enc_partial(float p) { return p >= 0.0f ? __float_as_uint(p) + 1u : 0u; }
+__device__ __forceinline__ float dec_partial(uint32_t e) { return e ? __uint_as_float(e - 1u) : -INFINITY; }
+
 __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
     return (uint32_t)(a & 0xff) | ((uint32_t)(b & 0xff) << 8) | ((uint32_t)(c & 0xff) << 16) |
            ((uint32_t)(d & 0xff) << 24);
@@ -42,14 +49,13 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 // ------------------------------------------------------------------------------------------------
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
 // R > 0: each lane keeps R float4 chunks in registers (len <= 256*R), one HBM read.
-// R == 0: two streaming passes (second pass mostly L2 hits).
+// R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
 template <int R>
-__global__ __launch_bounds__(256) void pack_rows_vec_kernel(const float *__restrict__ src, int64_t sh, int rows,
-                                                            int len, float range, float *__restrict__ scale,
-                                                            int8_t *__restrict__ q, int64_t rows_pad,
-                                                            int64_t k_pad) {
+__device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
+                                                   int len, float range, float *__restrict__ scale,
+                                                   int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = blk * 4 + (threadIdx.x >> 6);
     if (row >= rows_pad) return;
     uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
     const int64_t nq = k_pad >> 2;  // uint32 words per packed row
@@ -120,6 +126,14 @@ __global__ __launch_bounds__(256) void pack_rows_vec_kernel(const float *__restr
     if (lane == 0) scale[row] = cx;
 }
 
+template <int R>
+__global__ __launch_bounds__(256) void pack_rows_vec_kernel(const float *__restrict__ src, int64_t sh, int rows,
+                                                            int len, float range, float *__restrict__ scale,
+                                                            int8_t *__restrict__ q, int64_t rows_pad,
+                                                            int64_t k_pad) {
+    pack_rows_vec_body<R>(blockIdx.x, src, sh, rows, len, range, scale, q, rows_pad, k_pad);
+}
+
 // pack_rows, generic strides (any sh, sw): scalar loads, two passes.
 __global__ __launch_bounds__(256) void pack_rows_generic_kernel(const float *__restrict__ src, int64_t sh,
                                                                 int64_t sw, int rows, int len, float range,
@@ -146,55 +160,91 @@ __global__ __launch_bounds__(256) void pack_rows_generic_kernel(const float *__r
 }
 
 // ------------------------------------------------------------------------------------------------
-// pack_cols pass 1: per-column max of |x| over rows 1..len-1 of a [len x cols] row-major matrix
-// (row stride sh, unit column stride).  The seed row 0 is combined in pass 2.  Candidates are
-// non-negative and NaN-free, so float order == uint order of (bits + 1); 0 encodes "no candidate".
-constexpr int kColStrip = 1024;  // columns per block (256 threads x float4)
-constexpr int kColRows = 64;     // rows per block
+// pack_cols pass 1: for a [len x cols] row-major matrix (row stride sh, unit column stride), block
+// (cb, part) reduces |x| over rows [1 + 256*part, 1 + 256*(part+1)) of columns [256*cb, 256*cb+256)
+// (row 0 is the seed, combined in pass 2) and writes partial[part][col].  4 waves x 64 rows; each
+// lane owns 4 columns (VEC: contiguous float4 -> 1 KiB per wave load; else stride-64 scalars).
+constexpr int kColBlock = 256;  // columns per pass-1 block
+
+template <bool VEC>
+__device__ __forceinline__ void colmax_body(int cb, int part, const float *__restrict__ src, int64_t sh, int len,
+                                            int cols, uint32_t *__restrict__ partial, int64_t rows_pad,
+                                            float *red /* 4 x 256 floats of LDS */) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t r0 = 1 + (int64_t)part * kColChunk + w * 64;
+    const int64_t r1 = min((int64_t)len, r0 + 64);
+    const int64_t c0 = (int64_t)cb * kColBlock;
+    float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
+    if constexpr (VEC) {
+        const int64_t c = c0 + lane * 4;
+        if (c < cols) {
+            const float *base = src + c;
+#pragma unroll 8
+            for (int64_t r = r0; r < r1; ++r) {
+                const float4 x = *reinterpret_cast<const float4 *>(base + r * sh);
+                p0 = cand_max(p0, x.x);
+                p1 = cand_max(p1, x.y);
+                p2 = cand_max(p2, x.z);
+                p3 = cand_max(p3, x.w);
+            }
+        }
+        red[w * 256 + lane * 4 + 0] = p0;
+        red[w * 256 + lane * 4 + 1] = p1;
+        red[w * 256 + lane * 4 + 2] = p2;
+        red[w * 256 + lane * 4 + 3] = p3;
+    } else {
+        float pv[4] = {p0, p1, p2, p3};
+        for (int64_t r = r0; r < r1; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t c = c0 + lane + 64 * j;
+                if (c < cols) pv[j] = cand_max(pv[j], src[r * sh + c]);
+            }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[w * 256 + lane + 64 * j] = pv[j];
+    }
+    __syncthreads();
+    const int t = threadIdx.x;  // column within the block
+    float m = red[t];
+    m = fmaxf(m, red[256 + t]);  // all values are -inf or >= +0: fmaxf is exact here
+    m = fmaxf(m, red[512 + t]);
+    m = fmaxf(m, red[768 + t]);
+    if (c0 + t < cols) partial[(int64_t)part * rows_pad + c0 + t] = enc_partial(m);
+}
 
 template <bool VEC>
 __global__ __launch_bounds__(256) void colmax_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
-                                                     uint32_t *__restrict__ colmax) {
-    const int64_t r0 = 1 + (int64_t)blockIdx.y * kColRows;
-    const int64_t r1 = min((int64_t)len, r0 + kColRows);
-    if constexpr (VEC) {
-        const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-        if (c >= cols) return;
-        float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
-        const float *base = src + c;
-#pragma unroll 8
-        for (int64_t r = r0; r < r1; ++r) {
-            float4 x = *reinterpret_cast<const float4 *>(base + r * sh);
-            p0 = cand_max(p0, x.x);
-            p1 = cand_max(p1, x.y);
-            p2 = cand_max(p2, x.z);
-            p3 = cand_max(p3, x.w);
-        }
-        if (p0 >= 0.f) atomicMax(colmax + c + 0, __float_as_uint(p0) + 1u);
-        if (p1 >= 0.f) atomicMax(colmax + c + 1, __float_as_uint(p1) + 1u);
-        if (p2 >= 0.f) atomicMax(colmax + c + 2, __float_as_uint(p2) + 1u);
-        if (p3 >= 0.f) atomicMax(colmax + c + 3, __float_as_uint(p3) + 1u);
+                                                     uint32_t *__restrict__ partial, int64_t rows_pad) {
+    __shared__ float red[4 * 256];
+    colmax_body<VEC>(blockIdx.x, blockIdx.y, src, sh, len, cols, partial, rows_pad, red);
+}
+
+// Fused: blocks [0, ncol) run pass 1 of pack_cols(B), blocks [ncol, ncol + nrow) run pack_rows(A).
+template <int R>
+__global__ __launch_bounds__(256) void pack_rows_and_colmax_kernel(
+    const float *__restrict__ a, int64_t ash, int m, int k, float *__restrict__ a_scale, int8_t *__restrict__ a_q,
+    int64_t a_rows_pad, int64_t k_pad, const float *__restrict__ b, int64_t bsh, int n,
+    uint32_t *__restrict__ b_partial, int64_t b_rows_pad, int col_blocks, int ncol, float range) {
+    __shared__ float red[4 * 256];
+    const int bid = blockIdx.x;
+    if (bid < ncol) {
+        colmax_body<true>(bid % col_blocks, bid / col_blocks, b, bsh, k, n, b_partial, b_rows_pad, red);
     } else {
-        for (int64_t c = (int64_t)blockIdx.x * kColStrip + threadIdx.x; c < min((int64_t)cols, (int64_t)(blockIdx.x + 1) * kColStrip);
-             c += 256) {
-            float p = -INFINITY;
-            for (int64_t r = r0; r < r1; ++r) p = cand_max(p, src[r * sh + c]);
-            if (p >= 0.f) atomicMax(colmax + c, __float_as_uint(p) + 1u);
-        }
+        pack_rows_vec_body<R>(bid - ncol, a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad);
     }
 }
 
-// pack_cols pass 2: finish the column scale, quantize, transpose a [128 k][64 col] tile through LDS
-// and write 64 packed rows x 128 bytes.  Grid: (rows_pad/64, k_pad/128).
+// pack_cols pass 2: finish the column scale from the partials, quantize, transpose a [128 k][64 col]
+// tile through LDS and write 64 packed rows x 128 bytes.  Grid: (rows_pad/64, k_pad/128).
 constexpr int kTc = 64;             // output rows (= input columns) per block
 constexpr int kTk = 128;            // k per block
 constexpr int kTStride = kTk + 16;  // LDS row stride (bytes), keeps 16-B alignment
 
 template <bool VEC>
 __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
-                                                        float range, const uint32_t *__restrict__ colmax,
-                                                        float *__restrict__ scale, int8_t *__restrict__ q,
-                                                        int64_t k_pad) {
+                                                        float range, const uint32_t *__restrict__ partial,
+                                                        int64_t parts, int64_t rows_pad, float *__restrict__ scale,
+                                                        int8_t *__restrict__ q, int64_t k_pad) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[kTc * kTStride];
     __shared__ float s_sh[kTc];
     const int t = threadIdx.x;
@@ -204,8 +254,9 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
         const int64_t j = n0 + t;
         float cx = 0.0f, s = 0.0f;
         if (j < cols) {
-            const uint32_t e = colmax[j];
-            const float p = e ? __uint_as_float(e - 1u) : -INFINITY;
+            float p = -INFINITY;
+#pragma unroll 16
+            for (int64_t part = 0; part < parts; ++part) p = fmaxf(p, dec_partial(partial[part * rows_pad + j]));
             cx = absmax_finish(src[j], p);  // seed = row 0 (op_reduction.cuh:105)
             s = inv_divide(range, cx);
         }
@@ -217,29 +268,36 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
     const int rg = t >> 4;    // rows k0 + 4*rg + 64*h + {0..3}
     const float s0 = s_sh[4 * col4 + 0], s1 = s_sh[4 * col4 + 1], s2 = s_sh[4 * col4 + 2], s3 = s_sh[4 * col4 + 3];
     const int64_t c = n0 + 4 * col4;
+    float4 x[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t kk = k0 + 4 * rg + 64 * h + i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (kk < len) {
+                const float *rp = src + kk * sh + c;
+                if constexpr (VEC) {
+                    if (c < cols) v = *reinterpret_cast<const float4 *>(rp);
+                } else {
+                    if (c + 0 < cols) v.x = rp[0];
+                    if (c + 1 < cols) v.y = rp[1];
+                    if (c + 2 < cols) v.z = rp[2];
+                    if (c + 3 < cols) v.w = rp[3];
+                }
+            }
+            x[h][i] = v;
+        }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         int qv[4][4];  // [row i][col e]
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t kk = k0 + 4 * rg + 64 * h + i;
-            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (kk < len) {
-                const float *rp = src + kk * sh + c;
-                if constexpr (VEC) {
-                    if (c < cols) x = *reinterpret_cast<const float4 *>(rp);
-                } else {
-                    if (c + 0 < cols) x.x = rp[0];
-                    if (c + 1 < cols) x.y = rp[1];
-                    if (c + 2 < cols) x.z = rp[2];
-                    if (c + 3 < cols) x.w = rp[3];
-                }
-            }
-            // padding columns have s = 0 -> 0*x = 0 (x finite or zero-filled); force 0 anyway
-            qv[i][0] = (kk < len && c + 0 < cols) ? quant_i8(x.x, s0) : 0;
-            qv[i][1] = (kk < len && c + 1 < cols) ? quant_i8(x.y, s1) : 0;
-            qv[i][2] = (kk < len && c + 2 < cols) ? quant_i8(x.z, s2) : 0;
-            qv[i][3] = (kk < len && c + 3 < cols) ? quant_i8(x.w, s3) : 0;
+            qv[i][0] = (kk < len && c + 0 < cols) ? quant_i8(x[h][i].x, s0) : 0;
+            qv[i][1] = (kk < len && c + 1 < cols) ? quant_i8(x[h][i].y, s1) : 0;
+            qv[i][2] = (kk < len && c + 2 < cols) ? quant_i8(x[h][i].z, s2) : 0;
+            qv[i][3] = (kk < len && c + 3 < cols) ? quant_i8(x[h][i].w, s3) : 0;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -247,8 +305,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
                 pack4(qv[0][e], qv[1][e], qv[2][e], qv[3][e]);
     }
     __syncthreads();
-    const int n = t >> 2;          // packed row within the tile
-    const int kc = (t & 3) * 32;   // byte offset within the 128-byte k slice
+    const int n = t >> 2;         // packed row within the tile
+    const int kc = (t & 3) * 32;  // byte offset within the 128-byte k slice
     const uint4 *lp = reinterpret_cast<const uint4 *>(tile + n * kTStride + kc);
     uint4 *gp = reinterpret_cast<uint4 *>(q + (n0 + n) * k_pad + k0 + kc);
     gp[0] = lp[0];
@@ -268,45 +326,65 @@ __global__ __launch_bounds__(256) void fill_uniform_kernel(float *__restrict__ d
     }
 }
 
+bool rows_vec_ok(const float *src, int64_t sh, int64_t sw, int rows) {
+    return sw == 1 && (sh % 4 == 0 || rows == 1) && (reinterpret_cast<uintptr_t>(src) % 16 == 0);
+}
+
+bool cols_vec_ok(const float *src, int64_t sh, int cols) {
+    return (cols % 4 == 0) && (sh % 4 == 0) && (reinterpret_cast<uintptr_t>(src) % 16 == 0);
+}
+
+int rows_regs(int len) {  // float4 chunks per lane -> register-resident variant (0 = streaming)
+    const int per_lane = ((len >> 2) + 63) / 64;
+    return per_lane <= 1 ? 1 : per_lane <= 2 ? 2 : per_lane <= 4 ? 4 : per_lane <= 8 ? 8 : per_lane <= 16 ? 16 : 0;
+}
+
 }  // namespace
 
 hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, int len, float range, PackedView out,
                             hipStream_t stream) {
     const dim3 grid((unsigned)(out.rows_pad / 4)), block(256);
-    const bool vec = sw == 1 && (sh % 4 == 0 || rows == 1) && (reinterpret_cast<uintptr_t>(src) % 16 == 0);
-    if (!vec) {
+    if (!rows_vec_ok(src, sh, sw, rows)) {
         pack_rows_generic_kernel<<<grid, block, 0, stream>>>(src, sh, sw, rows, len, range, out.scale, out.q,
                                                              out.rows_pad, out.k_pad);
         return hipGetLastError();
     }
-    const int per_lane = ((len >> 2) + 63) / 64;  // float4 chunks per lane
 #define QG_ROWS(Rv) pack_rows_vec_kernel<Rv><<<grid, block, 0, stream>>>(src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad)
-    if (per_lane <= 1) QG_ROWS(1);
-    else if (per_lane <= 2) QG_ROWS(2);
-    else if (per_lane <= 4) QG_ROWS(4);
-    else if (per_lane <= 8) QG_ROWS(8);
-    else if (per_lane <= 16) QG_ROWS(16);
-    else QG_ROWS(0);
+    switch (rows_regs(len)) {
+        case 1: QG_ROWS(1); break;
+        case 2: QG_ROWS(2); break;
+        case 4: QG_ROWS(4); break;
+        case 8: QG_ROWS(8); break;
+        case 16: QG_ROWS(16); break;
+        default: QG_ROWS(0); break;
+    }
 #undef QG_ROWS
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
+                                  hipStream_t stream) {
+    const dim3 g2((unsigned)(out.rows_pad / kTc), (unsigned)(out.k_pad / kTk));
+    const int64_t parts = len > 1 ? out.parts : 0;  // K = 1: no candidates, Cw = seed
+    if (cols_vec_ok(src, sh, cols))
+        pack_cols_kernel<true><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch, parts, out.rows_pad,
+                                                       out.scale, out.q, out.k_pad);
+    else
+        pack_cols_kernel<false><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch, parts, out.rows_pad,
+                                                        out.scale, out.q, out.k_pad);
     return hipGetLastError();
 }
 
 hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                             hipStream_t stream) {
-    uint32_t *colmax = out.scratch;
-    hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * (size_t)cols, stream);
-    if (e != hipSuccess) return e;
-    const bool vec = (cols % 4 == 0) && (sh % 4 == 0) && (reinterpret_cast<uintptr_t>(src) % 16 == 0);
     if (len > 1) {
-        const dim3 g1((unsigned)((cols + kColStrip - 1) / kColStrip), (unsigned)((len - 1 + kColRows - 1) / kColRows));
-        if (vec) colmax_kernel<true><<<g1, 256, 0, stream>>>(src, sh, len, cols, colmax);
-        else colmax_kernel<false><<<g1, 256, 0, stream>>>(src, sh, len, cols, colmax);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const dim3 g1((unsigned)((cols + kColBlock - 1) / kColBlock), (unsigned)out.parts);
+        if (cols_vec_ok(src, sh, cols)) colmax_kernel<true><<<g1, 256, 0, stream>>>(src, sh, len, cols, out.scratch, out.rows_pad);
+        else colmax_kernel<false><<<g1, 256, 0, stream>>>(src, sh, len, cols, out.scratch, out.rows_pad);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    const dim3 g2((unsigned)(out.rows_pad / kTc), (unsigned)(out.k_pad / kTk));
-    if (vec) pack_cols_kernel<true><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, colmax, out.scale, out.q, out.k_pad);
-    else pack_cols_kernel<false><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, colmax, out.scale, out.q, out.k_pad);
-    return hipGetLastError();
+    return launch_pack_cols_pass2(src, sh, len, cols, range, out, stream);
 }
 
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream) {
@@ -314,6 +392,29 @@ hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float l
     int64_t blocks = (count + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     fill_uniform_kernel<<<(unsigned)blocks, 256, 0, stream>>>(dst, count, seed, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,
+                                         int64_t bsh, int n, PackedView outb, float range, hipStream_t stream) {
+    if (k < 2 || !rows_vec_ok(a, ash, 1, m) || !cols_vec_ok(b, bsh, n)) return hipErrorNotSupported;
+    const int col_blocks = (n + kColBlock - 1) / kColBlock;
+    const int ncol = col_blocks * (int)outb.parts;
+    const int nrow = (int)(outa.rows_pad / 4);
+#define QG_FUSED(Rv)                                                                                            \
+    pack_rows_and_colmax_kernel<Rv><<<ncol + nrow, 256, 0, stream>>>(a, ash, m, k, outa.scale, outa.q,          \
+                                                                     outa.rows_pad, outa.k_pad, b, bsh, n,       \
+                                                                     outb.scratch, outb.rows_pad, col_blocks,    \
+                                                                     ncol, range)
+    switch (rows_regs(k)) {
+        case 1: QG_FUSED(1); break;
+        case 2: QG_FUSED(2); break;
+        case 4: QG_FUSED(4); break;
+        case 8: QG_FUSED(8); break;
+        case 16: QG_FUSED(16); break;
+        default: QG_FUSED(0); break;
+    }
+#undef QG_FUSED
     return hipGetLastError();
 }
 

@@ -12,28 +12,36 @@ constexpr int kKPad = 128;
 
 __host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
-// Layout of one packed operand buffer: [scale: rows_pad f32][scratch: rows_pad u32][q: rows_pad x k_pad i8].
-// The scratch words hold the column-absmax partials of pack_cols (pass 1 -> pass 2).
+// Column-absmax partials: pack_cols' pass 1 reduces chunks of kColChunk rows (k >= 1) and writes one
+// partial per (chunk, column); pass 2 reduces the partials.  No atomics, nothing to zero per call.
+constexpr int kColChunk = 256;
+__host__ __device__ inline int64_t colmax_parts(int64_t k) { return k > 1 ? (k - 1 + kColChunk - 1) / kColChunk : 1; }
+
+// Layout of one packed operand buffer:
+//   [scale: rows_pad f32][scratch: parts x rows_pad u32][q: rows_pad x k_pad i8]
+// The scratch holds pack_cols' column-absmax partials (pass 1 -> pass 2).
 struct PackedView {
     float *scale;       // rows_pad floats (Cx or Cw)
-    uint32_t *scratch;  // rows_pad words
+    uint32_t *scratch;  // parts x rows_pad words
     int8_t *q;          // rows_pad x k_pad
-    int64_t rows_pad, k_pad;
+    int64_t rows_pad, k_pad, parts;
 };
 
 inline PackedView packed_view(const void *base, int rows, int k) {
     PackedView v;
     v.rows_pad = round_up(rows, kRowPad);
     v.k_pad = round_up(k, kKPad);
+    v.parts = colmax_parts(k);
     char *p = static_cast<char *>(const_cast<void *>(base));
     v.scale = reinterpret_cast<float *>(p);
     v.scratch = reinterpret_cast<uint32_t *>(p + v.rows_pad * 4);
-    v.q = reinterpret_cast<int8_t *>(p + v.rows_pad * 8);
+    v.q = reinterpret_cast<int8_t *>(p + round_up(v.rows_pad * 4 * (1 + v.parts), 256));
     return v;
 }
 
 inline size_t packed_bytes(int rows, int k) {
-    return (size_t)round_up(rows, kRowPad) * 8 + (size_t)round_up(rows, kRowPad) * round_up(k, kKPad);
+    const int64_t rp = round_up(rows, kRowPad);
+    return (size_t)round_up(rp * 4 * (1 + colmax_parts(k)), 256) + (size_t)rp * round_up(k, kKPad);
 }
 
 // ---- the reference's per-element arithmetic, pinned to single IEEE operations ----------------
@@ -80,6 +88,12 @@ hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, 
                             PackedView out, hipStream_t stream);
 hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                             hipStream_t stream);
+// One launch: pack_rows of a row-major A (vector path) and pass 1 of pack_cols of a row-major B.
+// Returns hipErrorNotSupported when the layouts do not allow it (caller falls back).
+hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,
+                                       int64_t bsh, int n, PackedView outb, float range, hipStream_t stream);
+hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
+                                  hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
                                int m, int n, float inv_r2, hipStream_t stream);
@@ -88,5 +102,13 @@ hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Ac
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
                          int64_t csh, int64_t csw, int m, int n, int k, hipStream_t stream);
 const char *gemm_config_name();
+
+// Diagnostics: events to record exactly around the next GEMM kernel (hipExtLaunchKernelGGL), set
+// through qgemm_set_gemm_events() and consumed by one launch.  Thread-local.
+struct GemmEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+GemmEvents take_gemm_events();
+void set_gemm_events(hipEvent_t start, hipEvent_t stop);
 
 }  // namespace qgemm

@@ -43,12 +43,17 @@ def test_library_carries_gfx950_code_object(qg):
 def test_version_and_sizes_without_gpu(qg):
     L = qg.load()
     assert "gfx950" in qg.version()
-    # packed operand: [scale rows_pad*4][reserved rows_pad*4][rows_pad*k_pad]
-    assert L.qgemm_packed_size(4096, 4096) == 4096 * 8 + 4096 * 4096
-    assert L.qgemm_packed_size(1, 1) == 256 * 8 + 256 * 128
-    assert L.qgemm_packed_size(257, 129) == 512 * 8 + 512 * 256
+    # packed operand: [scale rows_pad*4][reserved parts*rows_pad*4][rows_pad*k_pad], parts = ceil((k-1)/256)
+    def size(rows, k):
+        rp = -(-rows // 256) * 256
+        kp = -(-k // 128) * 128
+        parts = -(-(k - 1) // 256) if k > 1 else 1
+        head = -(-(rp * 4 * (1 + parts)) // 256) * 256
+        return head + rp * kp
+    for rows, k in [(4096, 4096), (1, 1), (257, 129), (2048, 16384), (3, 2)]:
+        assert L.qgemm_packed_size(rows, k) == size(rows, k), (rows, k)
     ws = L.op_mm_quantize_workspace_size(4096, 4096, 4096)
-    assert ws == 2 * (4096 * 8 + 4096 * 4096)
+    assert ws == 2 * size(4096, 4096)
     assert L.op_mm_quantize_workspace_size(4, 4, 0) == 0
 
 
