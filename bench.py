@@ -53,6 +53,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--gather", action="store_true", help="also time the whole-node all-gather of C (N>1)")
+    p.add_argument("--gemm-timing-every", type=int, default=5,
+                   help="time the GEMM kernel on every n-th timed step (events cost ~4 us per timed step)")
+    p.add_argument("--gemm-timing", default="ext", choices=["record", "ext", "none"],
+                   help="how the GEMM kernel is timed inside the timed region: hipExtLaunchKernel start/stop "
+                        "events (ext, exact kernel bounds), hipEventRecord around its launch (record, includes the "
+                        "kernel-boundary gap), or not at all (none)")
     return p.parse_args()
 
 
@@ -81,6 +87,22 @@ class HipEvents:
         for h in self.ev:
             self.hip.hipEventDestroy(h)
         self.ev = []
+
+
+def pmc_traffic(config):
+    """HBM bytes per GEMM launch from the newest committed PMC summary of this config
+    (profiles/rNN_pmc_<config>.json, written by scripts/summarize_pmc.py from separate
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 read correction), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{config}.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        g = d["kernels"]["gemm_i8"]
+        return g.get("hbm_bytes"), os.path.relpath(files[-1], REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def load_pkg():
@@ -149,10 +171,15 @@ def main():
     s = qg._stream(dev)
     range_ = 127.0
     hip = HipEvents(2 * args.steps)
+    L.qgemm_set_event_mode(1 if args.gemm_timing == "record" else 0)
+
+    mode = args.gemm_timing
+    every = max(1, args.gemm_timing_every)
+    timed = [i for i in range(args.steps) if i % every == 0]
 
     def step(i=None):
         # the drop-in call: op_mm_quantize on caller memory (explicit workspace, torch's stream)
-        if i is not None:  # time the GEMM kernel itself, exactly (hipExtLaunchKernel events)
+        if i is not None and mode != "none" and i % every == 0:
             L.qgemm_set_gemm_events(hip.ev[2 * i], hip.ev[2 * i + 1])
         rc = L.op_mm_quantize_ws(X.data_ptr(), K, 1, W.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, range_,
                                  ws.data_ptr(), ws.numel(), s)
@@ -173,7 +200,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    gemm_ms = sum(hip.elapsed_ms(hip.ev[2 * i], hip.ev[2 * i + 1]) for i in range(args.steps)) / args.steps
+    if mode != "none":
+        gemm_ms = sum(hip.elapsed_ms(hip.ev[2 * i], hip.ev[2 * i + 1]) for i in timed) / len(timed)
+    else:
+        gemm_ms = float("nan")
     hip.destroy()
     if distributed:
         t = torch.tensor([elapsed, gemm_ms], device=dev, dtype=torch.float64)
@@ -192,6 +222,7 @@ def main():
         del full
 
     ops = 2.0 * M * N * K
+    traffic, traffic_src = pmc_traffic(args.config)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * args.steps / elapsed
     achieved = ops / (gemm_ms * 1e-3) / 1e12
@@ -223,9 +254,14 @@ def main():
             "peak": round(PEAK_INT8_TOPS, 1),
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_INT8_TOPS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (HBM + Infinity Cache fill, FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "alg_bytes": M * K + N * K + 4 * M * N + 4 * (M + N),
             "kernel": "gemm_i8_v3<kStoreLds> (int8 16x16x64 MFMA GEMM + fused dequant epilogue)",
-            "timing": "hipExtLaunchKernel start/stop events on every GEMM launch of the timed steps",
+            "timing": {"record": "hipEventRecord right before/after the GEMM launch (same stream)",
+                       "ext": "hipExtLaunchKernel start/stop events on the GEMM launch",
+                       "none": "not timed"}[args.gemm_timing] + f" on {len(timed)} of the {args.steps} timed steps",
         },
         "library": qg.version(),
     }

@@ -97,6 +97,9 @@ QGEMM_API int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float
  * kernel of the NEXT op_mm_quantize* / qgemm_mm_packed call made by this thread (then cleared).
  * Used by bench.py to time the dominant kernel inside its timed region.  NULL, NULL = off. */
 QGEMM_API int qgemm_set_gemm_events(void *start_event, void *stop_event);
+/* How those events are taken: 0 = hipExtLaunchKernel start/stop (default), 1 = hipEventRecord on the
+ * stream right before / after the GEMM launch. */
+QGEMM_API int qgemm_set_event_mode(int mode);
 
 /* Library identification: "qgemm <version> gfx950 <kernel config>". */
 QGEMM_API const char *qgemm_version(void);

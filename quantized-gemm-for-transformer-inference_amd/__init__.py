@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "qgemm_mm_packed_i32",
     "qgemm_mm_fp32",
     "qgemm_set_gemm_events",
+    "qgemm_set_event_mode",
     "qgemm_fill_uniform",
     "qgemm_version",
 )
@@ -107,6 +108,8 @@ def load() -> ctypes.CDLL:
         L.qgemm_fill_uniform.restype = i32
         L.qgemm_set_gemm_events.argtypes = [vp, vp]
         L.qgemm_set_gemm_events.restype = i32
+        L.qgemm_set_event_mode.argtypes = [i32]
+        L.qgemm_set_event_mode.restype = i32
         L.qgemm_version.argtypes = []
         L.qgemm_version.restype = ctypes.c_char_p
         _lib = L

@@ -174,6 +174,12 @@ int qgemm_set_gemm_events(void *start_event, void *stop_event) {
     return 0;
 }
 
+int qgemm_set_event_mode(int mode) {
+    if (mode != 0 && mode != 1) return err(hipErrorInvalidValue);
+    set_gemm_event_mode(mode);
+    return 0;
+}
+
 int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, void *stream) {
     if (!dst || count < 0) return err(hipErrorInvalidValue);
     return err(launch_fill_uniform(dst, count, seed, lo, hi, static_cast<hipStream_t>(stream)));

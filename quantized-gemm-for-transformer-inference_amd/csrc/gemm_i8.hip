@@ -16,6 +16,8 @@ using namespace gemm;
 const char *gemm_config_name() { return "i8mfma16x16x64_t256x256x128_w8_glds2_ldsepi"; }
 
 static thread_local GemmEvents t_events;
+static int g_event_mode = 0;  // 0: hipExtLaunchKernel events, 1: hipEventRecord around the launch
+void set_gemm_event_mode(int mode) { g_event_mode = mode; }
 void set_gemm_events(hipEvent_t start, hipEvent_t stop) { t_events = GemmEvents{start, stop}; }
 GemmEvents take_gemm_events() {
     GemmEvents e = t_events;
@@ -33,12 +35,16 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
                inv_r2};
     const GemmEvents ev = take_gemm_events();
-    if (ev.start || ev.stop)
+    if ((ev.start || ev.stop) && g_event_mode == 0) {
         hipExtLaunchKernelGGL((gemm_i8_v3<kStoreLds, true, kPrio>), dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0,
                               stream, ev.start, ev.stop, 0, p);
-    else
-        gemm_i8_v3<kStoreLds, true, kPrio><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
-    return hipGetLastError();
+        return hipGetLastError();
+    }
+    if (ev.start) (void)hipEventRecord(ev.start, stream);
+    gemm_i8_v3<kStoreLds, true, kPrio><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
+    hipError_t e = hipGetLastError();
+    if (ev.stop) (void)hipEventRecord(ev.stop, stream);
+    return e;
 }
 
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n, hipStream_t stream) {

@@ -238,36 +238,22 @@ __global__ __launch_bounds__(256) void pack_rows_and_colmax_kernel(
 // tile through LDS and write 64 packed rows x 128 bytes.  Grid: (rows_pad/64, k_pad/128).
 constexpr int kTc = 64;             // output rows (= input columns) per block
 constexpr int kTk = 128;            // k per block
-constexpr int kTStride = kTk + 16;  // LDS row stride (bytes), keeps 16-B alignment
+constexpr int kTStride = kTk + 4;   // LDS row stride: 33 dwords (odd) -> transpose writes 2-way, reads conflict-free
 
 template <bool VEC>
 __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
                                                         float range, const uint32_t *__restrict__ partial,
                                                         int64_t parts, int64_t rows_pad, float *__restrict__ scale,
                                                         int8_t *__restrict__ q, int64_t k_pad) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kTc * kTStride];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kTc * kTStride];  // [64 packed rows][132 B]
     __shared__ float s_sh[kTc];
     const int t = threadIdx.x;
     const int64_t n0 = (int64_t)blockIdx.x * kTc;
     const int64_t k0 = (int64_t)blockIdx.y * kTk;
-    if (t < kTc) {
-        const int64_t j = n0 + t;
-        float cx = 0.0f, s = 0.0f;
-        if (j < cols) {
-            float p = -INFINITY;
-#pragma unroll 16
-            for (int64_t part = 0; part < parts; ++part) p = fmaxf(p, dec_partial(partial[part * rows_pad + j]));
-            cx = absmax_finish(src[j], p);  // seed = row 0 (op_reduction.cuh:105)
-            s = inv_divide(range, cx);
-        }
-        s_sh[t] = s;
-        if (blockIdx.y == 0) scale[j] = cx;
-    }
-    __syncthreads();
     const int col4 = t & 15;  // 4 input columns n0 + 4*col4 .. +3
     const int rg = t >> 4;    // rows k0 + 4*rg + 64*h + {0..3}
-    const float s0 = s_sh[4 * col4 + 0], s1 = s_sh[4 * col4 + 1], s2 = s_sh[4 * col4 + 2], s3 = s_sh[4 * col4 + 3];
     const int64_t c = n0 + 4 * col4;
+    // issue the tile loads first: their latency overlaps the column-scale reduction below
     float4 x[2][4];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -288,6 +274,21 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
             }
             x[h][i] = v;
         }
+    if (t < kTc) {
+        const int64_t j = n0 + t;
+        float cx = 0.0f, s = 0.0f;
+        if (j < cols) {
+            float p = -INFINITY;
+#pragma unroll 16
+            for (int64_t part = 0; part < parts; ++part) p = fmaxf(p, dec_partial(partial[part * rows_pad + j]));
+            cx = absmax_finish(src[j], p);  // seed = row 0 (op_reduction.cuh:105)
+            s = inv_divide(range, cx);
+        }
+        s_sh[t] = s;
+        if (blockIdx.y == 0) scale[j] = cx;
+    }
+    __syncthreads();
+    const float s0 = s_sh[4 * col4 + 0], s1 = s_sh[4 * col4 + 1], s2 = s_sh[4 * col4 + 2], s3 = s_sh[4 * col4 + 3];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         int qv[4][4];  // [row i][col e]
@@ -307,10 +308,10 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
     __syncthreads();
     const int n = t >> 2;         // packed row within the tile
     const int kc = (t & 3) * 32;  // byte offset within the 128-byte k slice
-    const uint4 *lp = reinterpret_cast<const uint4 *>(tile + n * kTStride + kc);
+    const uint32_t *lp = reinterpret_cast<const uint32_t *>(tile + n * kTStride + kc);  // 4-B aligned only
     uint4 *gp = reinterpret_cast<uint4 *>(q + (n0 + n) * k_pad + k0 + kc);
-    gp[0] = lp[0];
-    gp[1] = lp[1];
+    gp[0] = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+    gp[1] = make_uint4(lp[4], lp[5], lp[6], lp[7]);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -110,5 +110,6 @@ struct GemmEvents {
 };
 GemmEvents take_gemm_events();
 void set_gemm_events(hipEvent_t start, hipEvent_t stop);
+void set_gemm_event_mode(int mode);
 
 }  // namespace qgemm
