@@ -129,7 +129,11 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     // then W's quantize/transpose pass, then the GEMM -- three launches in all.
     if (a_stride_w == 1 && b_stride_w == 1 && k > 1) {
         const PackedView va = packed_view(pa, m, k), vb = packed_view(pb, n, k);
-        hipError_t e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
+        // K <= 4096: W read once (single-pass strips) -- two launches in all
+        hipError_t e = launch_pack_single_pass(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
+        if (e == hipSuccess) return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);
+        if (e != hipErrorNotSupported) return err(e);
+        e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
         if (e == hipSuccess) {
             if ((e = launch_pack_cols_pass2(B, b_stride_h, k, n, range, vb, s)) != hipSuccess) return err(e);
             return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);

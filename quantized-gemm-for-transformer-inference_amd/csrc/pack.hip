@@ -241,20 +241,8 @@ constexpr int kTk = 128;            // k per block
 constexpr int kTStride = kTk + 4;   // LDS row stride: 33 dwords (odd) -> transpose writes 2-way, reads conflict-free
 
 template <bool VEC>
-__global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
-                                                        float range, const uint32_t *__restrict__ partial,
-                                                        int64_t parts, int64_t rows_pad, float *__restrict__ scale,
-                                                        int8_t *__restrict__ q, int64_t k_pad) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kTc * kTStride];  // [64 packed rows][132 B]
-    __shared__ float s_sh[kTc];
-    const int t = threadIdx.x;
-    const int64_t n0 = (int64_t)blockIdx.x * kTc;
-    const int64_t k0 = (int64_t)blockIdx.y * kTk;
-    const int col4 = t & 15;  // 4 input columns n0 + 4*col4 .. +3
-    const int rg = t >> 4;    // rows k0 + 4*rg + 64*h + {0..3}
-    const int64_t c = n0 + 4 * col4;
-    // issue the tile loads first: their latency overlaps the column-scale reduction below
-    float4 x[2][4];
+__device__ __forceinline__ void load_col_tile(float4 (&x)[2][4], const float *__restrict__ src, int64_t sh, int len,
+                                              int cols, int64_t c, int64_t k0, int rg) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -274,6 +262,31 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
             }
             x[h][i] = v;
         }
+}
+
+// Block = 64 output rows (input columns) x kTilesPerBlock k-tiles of 128: the column scales are
+// computed once, and tile kt+1's loads are in flight while tile kt is quantized, transposed and
+// stored.  Grid: (rows_pad/64, ceil(k_pad/128 / kTilesPerBlock)).
+constexpr int kTilesPerBlock = 4;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
+                                                        float range, const uint32_t *__restrict__ partial,
+                                                        int64_t parts, int64_t rows_pad, float *__restrict__ scale,
+                                                        int8_t *__restrict__ q, int64_t k_pad) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[2][kTc * kTStride];  // [64 packed rows][132 B], 2 buffers
+    __shared__ float s_sh[kTc];
+    const int t = threadIdx.x;
+    const int64_t n0 = (int64_t)blockIdx.x * kTc;
+    const int64_t nkt = k_pad / kTk;
+    const int64_t kt0 = (int64_t)blockIdx.y * kTilesPerBlock;
+    const int64_t kt1 = min(nkt, kt0 + kTilesPerBlock);
+    const int col4 = t & 15;  // 4 input columns n0 + 4*col4 .. +3
+    const int rg = t >> 4;    // rows k0 + 4*rg + 64*h + {0..3}
+    const int64_t c = n0 + 4 * col4;
+    // first tile's loads before the scale reduction (their latency overlaps it)
+    float4 x[2][4], xn[2][4];
+    load_col_tile<VEC>(x, src, sh, len, cols, c, kt0 * kTk, rg);
     if (t < kTc) {
         const int64_t j = n0 + t;
         float cx = 0.0f, s = 0.0f;
@@ -289,29 +302,163 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
     }
     __syncthreads();
     const float s0 = s_sh[4 * col4 + 0], s1 = s_sh[4 * col4 + 1], s2 = s_sh[4 * col4 + 2], s3 = s_sh[4 * col4 + 3];
+    const int n = t >> 2;         // packed row within the tile (write-out role)
+    const int kc = (t & 3) * 32;  // byte offset within the 128-byte k slice
+    for (int64_t kt = kt0; kt < kt1; ++kt) {
+        const int64_t k0 = kt * kTk;
+        if (kt + 1 < kt1) load_col_tile<VEC>(xn, src, sh, len, cols, c, k0 + kTk, rg);
+        uint8_t *tb = tile[(kt - kt0) & 1];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        int qv[4][4];  // [row i][col e]
+        for (int h = 0; h < 2; ++h) {
+            int qv[4][4];  // [row i][col e]
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t kk = k0 + 4 * rg + 64 * h + i;
-            qv[i][0] = (kk < len && c + 0 < cols) ? quant_i8(x[h][i].x, s0) : 0;
-            qv[i][1] = (kk < len && c + 1 < cols) ? quant_i8(x[h][i].y, s1) : 0;
-            qv[i][2] = (kk < len && c + 2 < cols) ? quant_i8(x[h][i].z, s2) : 0;
-            qv[i][3] = (kk < len && c + 3 < cols) ? quant_i8(x[h][i].w, s3) : 0;
+            for (int i = 0; i < 4; ++i) {
+                const int64_t kk = k0 + 4 * rg + 64 * h + i;
+                qv[i][0] = (kk < len && c + 0 < cols) ? quant_i8(x[h][i].x, s0) : 0;
+                qv[i][1] = (kk < len && c + 1 < cols) ? quant_i8(x[h][i].y, s1) : 0;
+                qv[i][2] = (kk < len && c + 2 < cols) ? quant_i8(x[h][i].z, s2) : 0;
+                qv[i][3] = (kk < len && c + 3 < cols) ? quant_i8(x[h][i].w, s3) : 0;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                *reinterpret_cast<uint32_t *>(tb + (4 * col4 + e) * kTStride + 4 * rg + 64 * h) =
+                    pack4(qv[0][e], qv[1][e], qv[2][e], qv[3][e]);
         }
+        __syncthreads();  // tile tb complete (and, double-buffered, the other one is free to rewrite next)
+        const uint32_t *lp = reinterpret_cast<const uint32_t *>(tb + n * kTStride + kc);  // 4-B aligned only
+        uint4 *gp = reinterpret_cast<uint4 *>(q + (n0 + n) * k_pad + k0 + kc);
+        gp[0] = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+        gp[1] = make_uint4(lp[4], lp[5], lp[6], lp[7]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-            *reinterpret_cast<uint32_t *>(tile + (4 * col4 + e) * kTStride + 4 * rg + 64 * h) =
-                pack4(qv[0][e], qv[1][e], qv[2][e], qv[3][e]);
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[h][i] = xn[h][i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Single-pass packing for the common shapes (row-major X and W, K <= 4096, N % 16 == 0), ONE launch
+// of 1024-thread blocks with two roles:
+//   W strip (blocks [0, n/16)): 16 columns x all K rows of W held in registers (16 float4 per
+//       thread), column absmax reduced on chip (shuffle + LDS), scales computed, quantized from the
+//       registers, transposed through a [16][k_pad] byte image in LDS, written as 16 packed rows.
+//       W is read from HBM exactly once (the two-pass path reads it twice).
+//   X rows (remaining blocks): one wave per row, 16 rows per block (pack_rows_vec_body<16>).
+// Thread t of a W strip: c4 = t & 3 (columns n0 + 4*c4 .. +3), rq = t >> 2 (0..255): rows
+// 4*rq + e + 1024*i (e, i = 0..3); one wave instruction reads 16 rows x 64 B.
+constexpr int kWsCols = 16;
+constexpr int kWsMaxK = 4096;
+
+__device__ __forceinline__ void pack_w_strip_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
+                                                  int n, float range, float *__restrict__ scale,
+                                                  int8_t *__restrict__ q, int64_t k_pad, uint8_t *lds) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int c4 = t & 3, rq = t >> 2;
+    const int64_t n0 = (int64_t)strip * kWsCols;
+    float *red = reinterpret_cast<float *>(lds);                 // [16 waves][16 cols]
+    float *s_sh = red + 16 * 16;                                 // [16] scales
+    uint8_t *img = lds + 4096;                                   // [16 rows][k_pad + 16 bytes]
+    const int64_t istride = k_pad + 16;                          // breaks the 4-way write conflict
+    float4 v[4][4];                                              // [i][e]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 1024 * i;
+            v[i][e] = (r < k) ? *reinterpret_cast<const float4 *>(w + (int64_t)r * wsh + n0 + 4 * c4)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    // column candidates over rows >= 1 (row 0 is the seed)
+    float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 1024 * i;
+            if (r >= 1 && r < k) {
+                p0 = cand_max(p0, v[i][e].x);
+                p1 = cand_max(p1, v[i][e].y);
+                p2 = cand_max(p2, v[i][e].z);
+                p3 = cand_max(p3, v[i][e].w);
+            }
+        }
+    // reduce over the 16 lanes of the wave with the same c4 (lane bits 2..5), then over the 16 waves
+#pragma unroll
+    for (int off = 4; off < 64; off <<= 1) {
+        p0 = fmaxf(p0, __shfl_xor(p0, off, 64));
+        p1 = fmaxf(p1, __shfl_xor(p1, off, 64));
+        p2 = fmaxf(p2, __shfl_xor(p2, off, 64));
+        p3 = fmaxf(p3, __shfl_xor(p3, off, 64));
+    }
+    if (lane < 4) {
+        red[wv * 16 + 4 * lane + 0] = p0;
+        red[wv * 16 + 4 * lane + 1] = p1;
+        red[wv * 16 + 4 * lane + 2] = p2;
+        red[wv * 16 + 4 * lane + 3] = p3;
     }
     __syncthreads();
-    const int n = t >> 2;         // packed row within the tile
-    const int kc = (t & 3) * 32;  // byte offset within the 128-byte k slice
-    const uint32_t *lp = reinterpret_cast<const uint32_t *>(tile + n * kTStride + kc);  // 4-B aligned only
-    uint4 *gp = reinterpret_cast<uint4 *>(q + (n0 + n) * k_pad + k0 + kc);
-    gp[0] = make_uint4(lp[0], lp[1], lp[2], lp[3]);
-    gp[1] = make_uint4(lp[4], lp[5], lp[6], lp[7]);
+    if (t < kWsCols) {
+        float p = red[t];
+#pragma unroll
+        for (int ww = 1; ww < 16; ++ww) p = fmaxf(p, red[ww * 16 + t]);  // -inf or >= +0: exact
+        const float cw = absmax_finish(w[n0 + t], p);                   // seed = W[0, j]
+        s_sh[t] = inv_divide(range, cw);
+        scale[n0 + t] = cw;
+    }
+    __syncthreads();
+    const float s0 = s_sh[4 * c4 + 0], s1 = s_sh[4 * c4 + 1], s2 = s_sh[4 * c4 + 2], s3 = s_sh[4 * c4 + 3];
+    // quantize; 4 consecutive rows of one column -> one dword of the transposed image
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r0 = 4 * rq + 1024 * i;
+        if (r0 >= k_pad) continue;
+        int qv[4][4];  // [e][col]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool in = r0 + e < k;
+            qv[e][0] = in ? quant_i8(v[i][e].x, s0) : 0;
+            qv[e][1] = in ? quant_i8(v[i][e].y, s1) : 0;
+            qv[e][2] = in ? quant_i8(v[i][e].z, s2) : 0;
+            qv[e][3] = in ? quant_i8(v[i][e].w, s3) : 0;
+        }
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+            *reinterpret_cast<uint32_t *>(img + (int64_t)(4 * c4 + cc) * istride + r0) =
+                pack4(qv[0][cc], qv[1][cc], qv[2][cc], qv[3][cc]);
+    }
+    __syncthreads();
+    // write the 16 packed rows (k_pad bytes each) with 16-B stores
+    const int64_t words = (int64_t)kWsCols * k_pad / 16;
+    for (int64_t x = t; x < words; x += 1024) {
+        const int64_t row = x / (k_pad / 16), col16 = x % (k_pad / 16);
+        *reinterpret_cast<uint4 *>(q + (n0 + row) * k_pad + col16 * 16) =
+            *reinterpret_cast<const uint4 *>(img + row * istride + col16 * 16);
+    }
+}
+
+__global__ __launch_bounds__(1024) void pack_single_pass_kernel(
+    const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
+    int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
+    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    const int bid = blockIdx.x;
+    if (bid < nstrips) {
+        // blocks b and b+8 run on one XCD: give them adjacent strips, so each 128-B line of W (two
+        // 64-B strip segments) is fetched into that XCD's L2 once (bijective for any nstrips)
+        const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
+        const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        pack_w_strip_body(strip, w, wsh, k, n, range, w_scale, w_q, k_pad, dyn_lds);
+    } else if (bid < nstrips + (int)((w_rows_pad - n) / kWsCols)) {
+        // padding rows of packed W: zero rows, zero scales
+        const int64_t n0 = n + (int64_t)(bid - nstrips) * kWsCols;
+        for (int64_t i = threadIdx.x; i < (int64_t)kWsCols * k_pad / 16; i += 1024)
+            reinterpret_cast<uint4 *>(w_q + n0 * k_pad)[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x < kWsCols) w_scale[n0 + threadIdx.x] = 0.0f;
+    } else {
+        // X rows: 16 rows per 1024-thread block = four 4-row groups of the 256-thread body
+        const int64_t xb = bid - nstrips - (int)((w_rows_pad - n) / kWsCols);
+        pack_rows_vec_body<16>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad);  // rows 16xb + (t>>6)
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -365,7 +512,7 @@ hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, 
 
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream) {
-    const dim3 g2((unsigned)(out.rows_pad / kTc), (unsigned)(out.k_pad / kTk));
+    const dim3 g2((unsigned)(out.rows_pad / kTc), (unsigned)((out.k_pad / kTk + kTilesPerBlock - 1) / kTilesPerBlock));
     const int64_t parts = len > 1 ? out.parts : 0;  // K = 1: no candidates, Cw = seed
     if (cols_vec_ok(src, sh, cols))
         pack_cols_kernel<true><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch, parts, out.rows_pad,
@@ -386,6 +533,28 @@ hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, flo
         if (e != hipSuccess) return e;
     }
     return launch_pack_cols_pass2(src, sh, len, cols, range, out, stream);
+}
+
+hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
+                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream) {
+    if (k < 1 || k > kWsMaxK || n % kWsCols != 0 || !rows_vec_ok(x, xsh, 1, m) || !cols_vec_ok(w, wsh, n))
+        return hipErrorNotSupported;
+    const int nstrips = n / kWsCols;
+    const int npad = (int)((outw.rows_pad - n) / kWsCols);
+    const int nx = (int)(outx.rows_pad / 16);
+    const size_t lds = 4096 + (size_t)kWsCols * (outx.k_pad + 16);
+    static bool attr_set = false;  // dynamic LDS above 64 KiB must be allowed explicitly
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(pack_single_pass_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           4096 + kWsCols * (kWsMaxK + 16));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    pack_single_pass_kernel<<<nstrips + npad + nx, 1024, lds, stream>>>(x, xsh, m, k, outx.scale, outx.q, outx.rows_pad,
+                                                                         outx.k_pad, w, wsh, n, outw.scale, outw.q,
+                                                                         outw.rows_pad, nstrips, range);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream) {
