@@ -33,7 +33,7 @@ __global__ void to_tiled(const int8_t *src, int8_t *dst, int64_t rows, int64_t k
 }
 
 typedef void (*KernelFn)(GemmArgs);
-struct Variant { const char *name; KernelFn fn; bool check; bool tiled = false; };
+struct Variant { const char *name; KernelFn fn; bool check; bool tiled = false; int threads = kThreads; };
 
 int main(int argc, char **argv) {
     int m = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 4096;
@@ -73,6 +73,16 @@ int main(int argc, char **argv) {
         {"v3p_ns_novm", gemm_i8_v3<kStoreNone, true, kPrio | kNoVmWait>, false},
         {"v3p_ns_noglds", gemm_i8_v3<kStoreNone, true, kPrio | kNoGlds>, false},
         {"v3p_ns_nothing", gemm_i8_v3<kStoreNone, true, kPrio | kNoGlds | kNoBarrier | kNoVmWait>, false},
+        {"v7_lds", gemm_i8_v7<kStoreLds, false>, true},
+        {"v7_nostore", gemm_i8_v7<kStoreNone, false>, false},
+        {"v7d_lds", gemm_i8_v7<kStoreLds, true>, true},
+        {"v7d_nostore", gemm_i8_v7<kStoreNone, true>, false},
+        {"v9_lds", gemm_i8_v9<kStoreLds>, true, false, 256},
+        {"v9_nostore", gemm_i8_v9<kStoreNone>, false, false, 256},
+        {"v9t8_nostore", gemm_i8_v9<kStoreNone, 8>, false, false, 256},
+        {"v9t32_nostore", gemm_i8_v9<kStoreNone, 32>, false, false, 256},
+        {"v7e_lds", gemm_i8_v7<kStoreLds, false, 8, kV7Early>, true},
+        {"v7e_nostore", gemm_i8_v7<kStoreNone, false, 8, kV7Early>, false},
         {"v5_s3", gemm_i8_v5<3>, true},
         {"v6_s4_direct", gemm_i8_v6<4, kStoreDirect>, true},
         {"v6_s4_lds", gemm_i8_v6<4, kStoreLds>, true},
@@ -83,6 +93,46 @@ int main(int argc, char **argv) {
         {"v6t_s4_nostore", gemm_i8_v6<4, kStoreNone, true>, false, true},
         {"v6t_s3_nostore", gemm_i8_v6<3, kStoreNone, true>, false, true},
     };
+    // clock mode: build/gemm_lab m n k 0 clock -- per stamped variant, 2 s of back-to-back launches,
+    // then one stamped launch: in-kernel clock = d(memtime)/d(memrealtime) x 100 MHz (median over blocks)
+    if (only && std::string(only) == "clock") {
+        struct SV { const char *name; KernelFn fn; };
+        std::vector<SV> sv = {
+            {"v7_lds", gemm_i8_v7<kStoreLds, false, 8, kV7Stamp>},
+            {"v7_nostore", gemm_i8_v7<kStoreNone, false, 8, kV7Stamp>},
+            {"v7_noglds_ns", gemm_i8_v7<kStoreNone, false, 8, kV7Stamp | kV7NoGlds>},
+            {"v7e_lds", gemm_i8_v7<kStoreLds, false, 8, kV7Stamp | kV7Early>},
+            {"v7e_nostore", gemm_i8_v7<kStoreNone, false, 8, kV7Stamp | kV7Early>},
+        };
+        dim3 g(p.tiles_m * p.tiles_n), b(kThreads);
+        int nb = p.tiles_m * p.tiles_n;
+        for (auto &v : sv) {
+            hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
+            int launches = 0; float ms = 0;
+            CK(hipEventRecord(a));
+            while (ms < 2000) {
+                for (int i = 0; i < 200; ++i) v.fn<<<g, b>>>(p);
+                launches += 200;
+                CK(hipEventRecord(z)); CK(hipEventSynchronize(z)); CK(hipEventElapsedTime(&ms, a, z));
+            }
+            v.fn<<<g, b>>>(p);
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned long long> st((size_t)4096 * 6);
+            CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_stamp), st.size() * 8));
+            std::vector<double> loop_clk, epi_clk, loop_us, epi_us;
+            for (int i = 0; i < nb; ++i) {
+                const unsigned long long *s6 = &st[(size_t)i * 6];
+                loop_clk.push_back((double)(s6[2] - s6[0]) / (double)(s6[3] - s6[1]) * 0.1);
+                loop_us.push_back((double)(s6[3] - s6[1]) * 0.01);
+                epi_clk.push_back((double)(s6[4] - s6[2]) / std::max(1.0, (double)(s6[5] - s6[3])) * 0.1);
+                epi_us.push_back((double)(s6[5] - s6[3]) * 0.01);
+            }
+            auto med = [](std::vector<double> x) { std::sort(x.begin(), x.end()); return x[x.size() / 2]; };
+            printf("%-14s avg launch %7.2f us  loop: clock %.3f GHz, %6.2f us/block  epilogue: clock %.3f GHz, %6.2f us/block\n",
+                   v.name, ms * 1000 / launches, med(loop_clk), med(loop_us), med(epi_clk), med(epi_us));
+        }
+        return 0;
+    }
     if (only) {
         std::vector<Variant> keep;
         for (auto &v : vs)
@@ -92,14 +142,14 @@ int main(int argc, char **argv) {
     dim3 grid(p.tiles_m * p.tiles_n), block(kThreads);
     // reference output from v1_direct
     GemmArgs pr = p; pr.C = Cref;
-    vs[0].fn<<<grid, block>>>(pr);
+    vs[0].fn<<<grid, dim3(vs[0].threads)>>>(pr);
     CK(hipDeviceSynchronize());
     std::vector<float> href((size_t)m * n), hgot((size_t)m * n);
     CK(hipMemcpy(href.data(), Cref, href.size() * 4, hipMemcpyDeviceToHost));
     for (auto &v : vs) {
         if (!v.check) continue;
         CK(hipMemset(C, 0xff, (size_t)m * n * 4));
-        v.fn<<<grid, block>>>(v.tiled ? pt : p);
+        v.fn<<<grid, dim3(v.threads)>>>(v.tiled ? pt : p);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
         size_t bad = 0;
@@ -111,9 +161,9 @@ int main(int argc, char **argv) {
     for (int r = 0; r < rounds; ++r)
         for (size_t vi = 0; vi < vs.size(); ++vi) {
             const GemmArgs &pp = vs[vi].tiled ? pt : p;
-            for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, block>>>(pp);
+            for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, dim3(vs[vi].threads)>>>(pp);
             CK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, block>>>(pp);
+            for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, dim3(vs[vi].threads)>>>(pp);
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             t[vi].push_back(ms * 1000 / reps);

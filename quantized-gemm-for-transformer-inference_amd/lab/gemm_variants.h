@@ -2,6 +2,8 @@
 // library).  Results of each are recorded in DESIGN.md "GEMM experiments".
 #pragma once
 
+#include <type_traits>
+
 #include "../csrc/gemm_i8_kernels.h"
 
 namespace qgemm {
@@ -525,6 +527,318 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v6(GemmArgs p) {
             const int c4 = (tid & 63) * 4;
 #pragma unroll 4
             for (int rr = tid >> 6; rr < 128; rr += kThreads / 64) {
+                const int i = gi0 + half * 128 + rr;
+                if (i >= p.m) break;
+                const float4 v = *reinterpret_cast<const float4 *>(T + rr * BN + c4);
+                const int j = gj0 + c4;
+                if (full) {
+                    *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = v;
+                } else {
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+                }
+            }
+        }
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// v7: v3's schedule with the next sub-step's fragment reads interleaved INTO the current MFMA cluster
+// (sched_group_barrier: 2 MFMAs, 1 ds_read, ... then 8 MFMAs), so no read latency is exposed at the
+// cluster boundary and the compiler has no reason for a blanket lgkmcnt(0) before the cluster.
+// kDmaIn: also spread the next tile's 8 LDS-DMA issues over the first cluster.
+template <int kRest, int J>
+__device__ __forceinline__ void pin_reads() {
+    if constexpr (J < 12) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, (kRest * (J + 1)) / 12 - (kRest * J) / 12, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+        pin_reads<kRest, J + 1>();
+    }
+}
+
+// diagnostic in-kernel clock stamps (MI355X_MICROARCH.md 'DVFS give-back' item 6): per block,
+// s_memtime / s_memrealtime at kernel start, after the main loop, after the epilogue
+__device__ unsigned long long g_stamp[4096][6];
+enum V7Flags { kV7Stamp = 32, kV7NoGlds = 64, kV7Early = 128 };
+
+template <int kMode, bool kDmaIn, int kTail = 8, int kFlags = 0>
+__global__ __launch_bounds__(kThreads, 2) void gemm_i8_v7(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + 2048];
+    const int tid = threadIdx.x, lane = tid & 63;
+    if constexpr (kFlags & kV7Stamp)
+        if (tid == 0) {
+            g_stamp[blockIdx.x][0] = __builtin_amdgcn_s_memtime();
+            g_stamp[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+        }
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    int tm, tn;
+    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    Stager st;
+    st.init(p.A, p.B, tm, tn, p.k_pad, wave, lane);
+    const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
+    const int a_row0 = (wm * 128 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    int off[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+
+    v4i acc[8][4];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4i{};
+
+    auto read_frags = [&](v4i (&a)[8], v4i (&b)[4], int buf, int s) __attribute__((always_inline)) {
+        const int8_t *la = lds + buf * kStageBytes;
+        const int8_t *lb = la + kTileBytes;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[s]);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[s]);
+    };
+    // no s_setprio inside: it is a scheduling boundary and would fence the reads off the MFMAs
+    auto mfmas = [&](const v4i (&a)[8], const v4i (&b)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+    };
+    // pin the interleave: (32 - kTail) MFMAs paired with the 12 reads, then kTail MFMAs
+    auto pin = [&](auto dma_c) __attribute__((always_inline)) {
+        constexpr bool dma = decltype(dma_c)::value;
+        if constexpr (dma) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);
+            }
+        }
+        pin_reads<32 - kTail - (dma ? 8 : 0), 0>();
+        __builtin_amdgcn_sched_group_barrier(0x0008, kTail, 0);
+        __builtin_amdgcn_sched_barrier(0);  // nothing crosses into the next cluster
+    };
+
+    const int nk = (int)(p.k_pad / BK);
+    v4i a0[8], b0[4], a1[8], b1[4];
+    if constexpr (kFlags & kV7Early) {
+        // early staging: buffer cur is free at barrier B(kt) (every read of tile kt has retired), so
+        // tile kt+2 is issued right there and has a whole k-step to land (vs half a k-step)
+        st.stage(lds, 0, 0);
+        if (nk > 1) {
+            st.stage(lds, 1, 1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        read_frags(a0, b0, 0, 0);
+        for (int kt = 0; kt < nk - 1; ++kt) {
+            const int cur = kt & 1;
+            read_frags(a1, b1, cur, 1);
+            mfmas(a0, b0);
+            pin(std::false_type{});
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (kt + 2 < nk) st.stage(lds, kt + 2, cur);
+            read_frags(a0, b0, cur ^ 1, 0);
+            mfmas(a1, b1);
+            pin(std::false_type{});
+        }
+    } else {
+    st.stage(lds, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    read_frags(a0, b0, 0, 0);
+    // steady state: every k-step but the last stages the next tile (straight-line body, one block)
+    for (int kt = 0; kt < nk - 1; ++kt) {
+        const int cur = kt & 1;
+        if constexpr (!(kFlags & kV7NoGlds)) st.stage(lds, kt + 1, cur ^ 1);
+        read_frags(a1, b1, cur, 1);
+        mfmas(a0, b0);
+        pin(std::integral_constant<bool, kDmaIn && !(kFlags & kV7NoGlds)>{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        read_frags(a0, b0, cur ^ 1, 0);
+        mfmas(a1, b1);
+        pin(std::false_type{});
+    }
+    }
+    {
+        const int cur = (nk - 1) & 1;
+        read_frags(a1, b1, cur, 1);
+        mfmas(a0, b0);
+        pin(std::false_type{});
+        mfmas(a1, b1);
+    }
+    if constexpr (kFlags & kV7Stamp)
+        if (tid == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            g_stamp[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
+            g_stamp[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+        }
+
+    epilogue16<kMode>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+    if constexpr (kFlags & kV7Stamp)
+        if (tid == 0) {
+            g_stamp[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
+            g_stamp[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();
+        }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// v9: Tensile-style big wave tiles -- 4 waves (one per SIMD), 2x2, each 128x128 of the 256x256 tile
+// (acc 8x8 16x16 tiles = 256 regs, AGPR-resident).  LDS read bytes per MAC drop by a third vs the
+// 128x64 wave tile (1/128+1/128 vs 1/64+1/128).  Early staging and interleaved reads as in v7e.
+template <int kRest, int kReads, int J>
+__device__ __forceinline__ void pin_reads_n() {
+    if constexpr (J < kReads) {
+        __builtin_amdgcn_sched_group_barrier(0x0008, (kRest * (J + 1)) / kReads - (kRest * J) / kReads, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+        pin_reads_n<kRest, kReads, J + 1>();
+    }
+}
+
+template <int kMode, int kTail = 16, int kFlags = 0>
+__global__ __launch_bounds__(256, 1) void gemm_i8_v9(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + 2048];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int tm, tn;
+    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const int8_t *Ablk = p.A + (int64_t)tm * BM * p.k_pad;
+    const int8_t *Bblk = p.B + (int64_t)tn * BN * p.k_pad;
+    // wave w fills rows [64w, 64w+64) of both tiles, 8 rows (1 KiB) per glds, chunk-swizzled source
+    int src_off[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = wave * 64 + i * 8 + (lane >> 3);
+        const int g = (lane & 7) ^ ((row >> 1) & 7);
+        src_off[i] = row * (int)p.k_pad + g * 16;
+    }
+    auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
+        int8_t *la = lds + buf * kStageBytes;
+        int8_t *lb = la + kTileBytes;
+        const int8_t *ga = Ablk + (int64_t)kt * BK;
+        const int8_t *gb = Bblk + (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_global_load_lds((const void *)(ga + src_off[i]), (void *)(la + (wave * 64 + i * 8) * BK), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(gb + src_off[i]), (void *)(lb + (wave * 64 + i * 8) * BK), 16, 0, 0);
+        }
+    };
+    const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
+    const int a_row0 = (wm * 128 + lrow) * BK, b_row0 = (wn * 128 + lrow) * BK;
+    int off[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+
+    v4i acc[8][8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = v4i{};
+
+    auto read_frags = [&](v4i (&a)[8], v4i (&b)[8], int buf, int s) __attribute__((always_inline)) {
+        const int8_t *la = lds + buf * kStageBytes;
+        const int8_t *lb = la + kTileBytes;
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[s]);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[s]);
+    };
+    auto mfmas = [&](const v4i (&a)[8], const v4i (&b)[8]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+    };
+    auto pin = [&]() __attribute__((always_inline)) {
+        pin_reads_n<64 - kTail, 16, 0>();
+        __builtin_amdgcn_sched_group_barrier(0x0008, kTail, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    const int nk = (int)(p.k_pad / BK);
+    v4i a0[8], b0[8], a1[8], b1[8];
+    stage(0, 0);
+    if (nk > 1) {
+        stage(1, 1);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    read_frags(a0, b0, 0, 0);
+    for (int kt = 0; kt < nk - 1; ++kt) {
+        const int cur = kt & 1;
+        read_frags(a1, b1, cur, 1);
+        mfmas(a0, b0);
+        pin();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + 2 < nk) stage(kt + 2, cur);
+        read_frags(a0, b0, cur ^ 1, 0);
+        mfmas(a1, b1);
+        pin();
+    }
+    {
+        const int cur = (nk - 1) & 1;
+        read_frags(a1, b1, cur, 1);
+        mfmas(a0, b0);
+        pin();
+        mfmas(a1, b1);
+    }
+
+    // epilogue
+    const int gi0 = tm * BM, gj0 = tn * BN;
+    if constexpr (kMode == kStoreNone) {
+        int x = 0;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x ^= acc[mi][ni][r];
+        if (x == 0x7fffffff && p.m < 0) static_cast<int *>(p.C)[tid] = x;
+        return;
+    } else {
+        float *sCx = reinterpret_cast<float *>(lds + kLdsBytes);
+        float *sCw = sCx + BM;
+        float *C = static_cast<float *>(p.C);
+        __syncthreads();
+        sCx[tid] = p.Cx[gi0 + tid];
+        sCw[tid] = p.Cw[gj0 + tid];
+        float *T = reinterpret_cast<float *>(lds);  // [128][256] fp32
+        const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
+                          gj0 + BN <= p.n;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            __syncthreads();
+            if (wm == half) {
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni) {
+                    const int jl = wn * 128 + ni * 16 + lrow;
+                    const float cw = sCw[jl];
+#pragma unroll
+                    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int il = mi * 16 + 4 * kq + r;
+                            T[il * BN + jl] = dequantize(acc[mi][ni][r], outer_product(sCx[half * 128 + il], cw), p.inv_r2);
+                        }
+                }
+            }
+            __syncthreads();
+            const int c4 = (tid & 63) * 4;
+#pragma unroll 4
+            for (int rr = tid >> 6; rr < 128; rr += 4) {
                 const int i = gi0 + half * 128 + rr;
                 if (i >= p.m) break;
                 const float4 v = *reinterpret_cast<const float4 *>(T + rr * BN + c4);

@@ -18,7 +18,7 @@ from collections import defaultdict
 
 
 def short(name):
-    for key in ("gemm_i8", "pack_rows_and_colmax", "pack_cols", "pack_rows", "colmax", "fill_uniform"):
+    for key in ("gemm_i8", "pack_single_pass", "pack_rows_and_colmax", "pack_cols", "pack_rows", "colmax", "fill_uniform"):
         if key in name:
             return key
     return name[-40:]
@@ -64,6 +64,7 @@ def main():
         res[k] = r
     alg = {"gemm_i8": {"int8_ops": 2 * M * N * K,
                        "alg_bytes": M * K + N * K + 4 * M * N + 4 * (M + N)},
+           "pack_single_pass": {"alg_bytes": 4 * M * K + M * K + 4 * K * N + K * N + 4 * (M + N)},
            "pack_rows_and_colmax": {"alg_bytes": 4 * M * K + M * K + 4 * K * N},
            "pack_cols": {"alg_bytes": 4 * K * N + K * N}}
     for k, a in alg.items():
