@@ -6,6 +6,7 @@
 //   pack A  (Cx + X_int8)          -- op_mm.cuh:76-77, 82-83, 86-87
 //   pack B  (Cw + W_int8^T)        -- op_mm.cuh:78-79, 84-85, 88-89
 //   MFMA GEMM + dequant epilogue   -- op_mm.cuh:92-99
+#include <map>
 #include <mutex>
 #include <stdio.h>
 
@@ -66,6 +67,43 @@ hipError_t cached_workspace(size_t need, void **out) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Split-K scratch for qgemm_mm_packed (which has no workspace argument): grow-only, one per
+// (device, stream) -- the tickets and slabs are only safe to reuse in stream order.
+struct ScratchKey {
+    int dev;
+    hipStream_t stream;
+    bool operator<(const ScratchKey &o) const { return dev != o.dev ? dev < o.dev : stream < o.stream; }
+};
+std::mutex g_scratch_mu;
+std::map<ScratchKey, CachedWs> g_scratch;
+hipError_t cached_scratch(size_t need, hipStream_t stream, void **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    CachedWs &w = g_scratch[ScratchKey{dev, stream}];
+    if (w.bytes < need) {
+        if (w.ptr) {
+            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+            if ((e = hipFree(w.ptr)) != hipSuccess) return e;
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        if ((e = hipMalloc(&w.ptr, need)) != hipSuccess) return e;
+        w.bytes = need;
+    }
+    *out = w.ptr;
+    return hipSuccess;
+}
+
+hipError_t mm_packed_impl(const void *packed_a, const void *packed_b, float *C, int64_t c_stride_h,
+                          int64_t c_stride_w, int m, int n, int k, float range, void *scratch, size_t scratch_bytes,
+                          hipStream_t stream) {
+    const float inv_r2 = 1.0f / (range * range);  // op_mm.cuh:99, one rounding per operation (host IEEE)
+    return launch_gemm_dequant(packed_view(packed_a, m, k), packed_view(packed_b, n, k), C, c_stride_h, c_stride_w, m,
+                               n, inv_r2, scratch, scratch_bytes, stream);
+}
+
 }  // namespace
 
 extern "C" {
@@ -77,7 +115,8 @@ size_t qgemm_packed_size(int rows, int k) {
 
 size_t op_mm_quantize_workspace_size(int m, int n, int k) {
     if (!dims_ok(m, n, k)) return 0;
-    return align256(packed_bytes(m, k)) + align256(packed_bytes(n, k));
+    // [split-K scratch (0 unless the shape has too few tiles)][packed A][packed B]
+    return align256(gemm_scratch_bytes(m, n, k)) + align256(packed_bytes(m, k)) + align256(packed_bytes(n, k));
 }
 
 int qgemm_pack_a(const float *A, int64_t a_stride_h, int64_t a_stride_w, int m, int k, float range, void *packed_a,
@@ -102,9 +141,14 @@ int qgemm_mm_packed(const void *packed_a, const void *packed_b, float *C, int64_
                     int m, int n, int k, float range, void *stream) {
     if (!packed_a || !packed_b || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
     if (m == 0 || n == 0) return 0;
-    const float inv_r2 = 1.0f / (range * range);  // op_mm.cuh:99, one rounding per operation (host IEEE)
-    return err(launch_gemm_dequant(packed_view(packed_a, m, k), packed_view(packed_b, n, k), C, c_stride_h,
-                                   c_stride_w, m, n, inv_r2, static_cast<hipStream_t>(stream)));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    void *scratch = nullptr;
+    const size_t sb = gemm_scratch_bytes(m, n, k);
+    if (sb) {
+        hipError_t e = cached_scratch(sb, s, &scratch);
+        if (e != hipSuccess) return err(e);
+    }
+    return err(mm_packed_impl(packed_a, packed_b, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s));
 }
 
 int qgemm_mm_packed_i32(const void *packed_a, const void *packed_b, int32_t *Acc, int m, int n, int k, void *stream) {
@@ -122,21 +166,24 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     if (m == 0 || n == 0) return 0;
     const size_t need = op_mm_quantize_workspace_size(m, n, k);
     if (!workspace || ws_bytes < need) return err(hipErrorInvalidValue);
-    char *pa = static_cast<char *>(workspace);
+    char *scratch = static_cast<char *>(workspace);
+    const size_t sb = gemm_scratch_bytes(m, n, k);
+    char *pa = scratch + align256(sb);
     char *pb = pa + align256(packed_bytes(m, k));
     hipStream_t s = static_cast<hipStream_t>(stream);
+    auto gemm = [&]() { return err(mm_packed_impl(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s)); };
     // Common case (row-major X and W): X's row pass and W's column-absmax pass share one launch,
     // then W's quantize/transpose pass, then the GEMM -- three launches in all.
     if (a_stride_w == 1 && b_stride_w == 1 && k > 1) {
         const PackedView va = packed_view(pa, m, k), vb = packed_view(pb, n, k);
         // K <= 4096: W read once (single-pass strips) -- two launches in all
         hipError_t e = launch_pack_single_pass(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
-        if (e == hipSuccess) return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);
+        if (e == hipSuccess) return gemm();
         if (e != hipErrorNotSupported) return err(e);
         e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
         if (e == hipSuccess) {
             if ((e = launch_pack_cols_pass2(B, b_stride_h, k, n, range, vb, s)) != hipSuccess) return err(e);
-            return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);
+            return gemm();
         }
         if (e != hipErrorNotSupported) return err(e);
     }
@@ -144,7 +191,7 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     if (rc) return rc;
     rc = qgemm_pack_b(B, b_stride_h, b_stride_w, k, n, range, pb, stream);
     if (rc) return rc;
-    return qgemm_mm_packed(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, stream);
+    return gemm();
 }
 
 int op_mm_quantize_ex(const float *A, int64_t a_stride_h, int64_t a_stride_w, const float *B, int64_t b_stride_h,

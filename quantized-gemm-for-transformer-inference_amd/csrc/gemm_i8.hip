@@ -29,19 +29,52 @@ static bool shape_ok(const PackedView &a, const PackedView &b) {
     return a.k_pad == b.k_pad && a.rows_pad % BM == 0 && b.rows_pad % BN == 0 && a.k_pad % BK == 0;
 }
 
+// Slices per tile: enough blocks to cover the CUs (one 130-KiB-LDS block per CU), each slice at least
+// two k-steps, at most 8 slices.  Shapes with >= 160 tiles are not split.
+int gemm_splits(int m, int n, int k) {
+    if (m <= 0 || n <= 0 || k <= 0) return 1;
+    const int64_t tiles = (round_up(m, BM) / BM) * (round_up(n, BN) / BN);
+    const int nk = (int)(round_up(k, BK) / BK);
+    if (tiles >= 160) return 1;
+    int s = (int)(256 / tiles);
+    s = s < nk / 2 ? s : nk / 2;
+    s = s < 8 ? s : 8;
+    return s > 1 ? s : 1;
+}
+
+static size_t ticket_bytes(int64_t tiles) { return (size_t)round_up(tiles * 4, 256); }
+
+size_t gemm_scratch_bytes(int m, int n, int k) {
+    const int s = gemm_splits(m, n, k);
+    if (s <= 1) return 0;
+    const int64_t tiles = (round_up(m, BM) / BM) * (round_up(n, BN) / BN);
+    return ticket_bytes(tiles) + (size_t)tiles * s * kSlabInts * 4;
+}
+
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw, int m,
-                               int n, float inv_r2, hipStream_t stream) {
+                               int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
-               inv_r2};
+               inv_r2, 1, nullptr, nullptr};
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+    const int splits = gemm_splits(m, n, (int)a.k_pad);
+    if (splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
+        p.splits = splits;
+        p.tickets = static_cast<unsigned *>(scratch);
+        p.slabs = reinterpret_cast<int32_t *>(static_cast<char *>(scratch) + ticket_bytes(tiles));
+        // the tickets are polled state: zeroed ahead of every launch (a memset node under capture)
+        hipError_t e = hipMemsetAsync(p.tickets, 0, ticket_bytes(tiles), stream);
+        if (e != hipSuccess) return e;
+    }
+    const dim3 grid((unsigned)(tiles * p.splits));
     const GemmEvents ev = take_gemm_events();
     if ((ev.start || ev.stop) && g_event_mode == 0) {
-        hipExtLaunchKernelGGL((gemm_i8_v3<kStoreLds, true, kPrio>), dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0,
-                              stream, ev.start, ev.stop, 0, p);
+        hipExtLaunchKernelGGL((gemm_i8_v3<kStoreLds, true, kPrio>), grid, dim3(kThreads), 0, stream, ev.start, ev.stop,
+                              0, p);
         return hipGetLastError();
     }
     if (ev.start) (void)hipEventRecord(ev.start, stream);
-    gemm_i8_v3<kStoreLds, true, kPrio><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
+    gemm_i8_v3<kStoreLds, true, kPrio><<<grid, dim3(kThreads), 0, stream>>>(p);
     hipError_t e = hipGetLastError();
     if (ev.stop) (void)hipEventRecord(ev.stop, stream);
     return e;
@@ -50,7 +83,7 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n, hipStream_t stream) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, Acc, n, 1, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
-               0.0f};
+               0.0f, 1, nullptr, nullptr};
     gemm_i8_v1<kStoreDirect, false><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
     return hipGetLastError();
 }

@@ -32,9 +32,12 @@ enum StoreMode { kStoreDirect = 0, kStoreLds = 1, kStoreNone = 2 };
 // Block -> macro-tile.  Blocks b and b+8 are dispatched to the same XCD; give each XCD a contiguous
 // range of logical ids (bijective for any grid size), then walk logical ids in groups of kGroupM
 // tile-rows so one XCD's range covers a compact patch (shared A and B panels stay in its L2).
-__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int &tm, int &tn) {
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ void group_tiles(int wgid, int tiles_m, int tiles_n, int &tm, int &tn) {
     constexpr int kGroupM = 4;
     const int per_group = kGroupM * tiles_n;
     const int group = wgid / per_group;
@@ -43,6 +46,10 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
     const int w = wgid - group * per_group;
     tm = first_m + w % gsz;
     tn = w / gsz;
+}
+
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int &tm, int &tn) {
+    group_tiles(xcd_remap(bid, nwg), tiles_m, tiles_n, tm, tn);
 }
 
 struct GemmArgs {
@@ -56,7 +63,15 @@ struct GemmArgs {
     int64_t k_pad;
     int tiles_m, tiles_n;
     float inv_r2;
+    // split-K (splits > 1): slice s of a tile runs k-steps [s*nk/S, (s+1)*nk/S); every slice stores its
+    // int32 accumulators to slabs[tile][s] and draws a ticket; the last arriver sums the slabs (exact
+    // integer addition, so any split gives bit-identical results) and runs the epilogue.
+    int splits;
+    int32_t *slabs;     // tiles x splits x (BM x BN) int32, MFMA-native order
+    unsigned *tickets;  // tiles words, zeroed before every launch
 };
+
+constexpr int64_t kSlabInts = (int64_t)BM * BN;
 
 // ------------------------------------------------------------------------------------------------
 // Shared pieces
@@ -347,14 +362,63 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 // v3: as v2 but on v_mfma_i32_16x16x64_i8 (16 x 16 output per MFMA, 64-deep k).  Per wave 128 x 64 =
 // 8 x 4 tiles; per 64-deep sub-step 8 A + 4 B fragment reads (lane l: row l&15, 16 bytes of k-chunk
 // 4s + (l>>4)) and 32 MFMAs.  C/D map: col = lane&15, row = 4(lane>>4) + reg.
+// In-launch split-K combine (cdna_hip_programming.md s5 "In-launch split-K reduction", the counter
+// form of s6 Guideline 16): every slice stores its accumulators as a slab with plain 16-B stores,
+// drains, and after the block barrier lane 0 publishes with ONE agent-scope release and draws a
+// ticket; the slice that draws S-1 is the reducer: ONE agent-scope acquire, then plain slab loads.
+// Correct for any placement of a tile's slices over XCDs/CUs.  The "last arriver" word goes through
+// the one LDS array (a second __shared__ object can de-pipeline the main loop).  Returns true in the
+// reducer, which then holds the complete sums in acc.
+__device__ __forceinline__ bool splitk_combine(const GemmArgs &p, int8_t *lds, v4i (&acc)[8][4], int tile, int slice,
+                                               int S, int wave, int lane, int tid) {
+    v4i *slabs = reinterpret_cast<v4i *>(p.slabs) + (int64_t)tile * S * (kSlabInts / 4);
+    v4i *mine = slabs + (int64_t)slice * (kSlabInts / 4) + wave * (32 * 64) + lane;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) mine[(mi * 4 + ni) * 64] = acc[mi][ni];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned *last = reinterpret_cast<unsigned *>(lds + kLdsBytes);
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last = t;
+        if (t == (unsigned)(S - 1)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (*last != (unsigned)(S - 1)) return false;
+    for (int s = 0; s < S; ++s) {
+        if (s == slice) continue;
+        const v4i *src = slabs + (int64_t)s * (kSlabInts / 4) + wave * (32 * 64) + lane;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) acc[mi][ni] += src[(mi * 4 + ni) * 64];
+    }
+    return true;
+}
+
 template <int kMode, bool kDequant, int kFlags = 0>
 __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + 2048];  // + scales for the epilogue
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
+    // XCD remap first, then tile = id / S, slice = id % S: a tile's slices share an XCD (their slabs
+    // are read back at the same-XCD rate; placement is a speed choice only)
+    const int S = p.splits > 1 ? p.splits : 1;
+    const int wid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = wid / S, slice = wid - tile * S;
     int tm, tn;
-    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
+    const int nk_all = (int)(p.k_pad / BK);
+    const int kt0 = slice * nk_all / S;
+    const int nk = (slice + 1) * nk_all / S - kt0;
     Stager st;
     st.init(p.A, p.B, tm, tn, p.k_pad, wave, lane);
     const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
@@ -387,9 +451,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
         if constexpr (kFlags & kPrio) __builtin_amdgcn_s_setprio(0);
     };
 
-    const int nk = (int)(p.k_pad / BK);
     v4i a0[8], b0[4], a1[8], b1[4];
-    st.stage(lds, 0, 0);
+    st.stage(lds, kt0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     read_frags(a0, b0, 0, 0);
@@ -397,7 +460,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
         const int cur = kt & 1;
         const bool more = kt + 1 < nk;
         if (!(kFlags & kNoGlds) || kt == 0)
-            if (more) st.stage(lds, kt + 1, cur ^ 1);
+            if (more) st.stage(lds, kt0 + kt + 1, cur ^ 1);
         read_frags(a1, b1, cur, 1);
         mfmas(a0, b0);
         if constexpr (!(kFlags & kNoVmWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -407,6 +470,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
         mfmas(a1, b1);
     }
 
+    if (S > 1 && !splitk_combine(p, lds, acc, tile, slice, S, wave, lane, tid)) return;
     epilogue16<kMode>(p, lds, acc, tm, tn, wm, wn, lane, tid);
 }
 

@@ -99,8 +99,13 @@ hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, Pa
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
+// Split-K for shapes with too few 256x256 tiles to fill the chip: gemm_splits() slices per tile and
+// the scratch (tickets + int32 slabs) they need; 1 / 0 when the shape is not split.
+int gemm_splits(int m, int n, int k);
+size_t gemm_scratch_bytes(int m, int n, int k);
+// scratch: gemm_scratch_bytes(m, n, k) bytes, or nullptr (then no split: correct, slower)
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
-                               int m, int n, float inv_r2, hipStream_t stream);
+                               int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream);
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
                            hipStream_t stream);
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,

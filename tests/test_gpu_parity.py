@@ -83,6 +83,23 @@ def test_random_shapes_full_oracle(qg, oracle, device, M, N, K):
     assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 4096), (300, 520, 1000), (512, 1024, 2048)])
+def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
+    """Few-tile shapes run split-K (int32 slabs + arrival tickets, combined in-launch): exact integer
+    sums, so bit-identical to the oracle; repeated calls reuse the tickets (zeroed per launch) and
+    the slabs with caches warm from the previous call."""
+    X, W = oracle.inputs(M, N, K, 71)
+    want = oracle.quantized_mm(X, W)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    pa, pb = qg.pack_a(Xd), qg.pack_b(Wd)
+    for i in range(3):
+        O = torch.full((M, N), float("nan"), device=device)
+        qg.mm_packed(pa, pb, O)
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} mm_packed call {i}")
+    assert_bits_equal(_run_full(qg, X, W, device), want, f"{M}x{N}x{K} op_quantized_mm")
+
+
 def test_device_generator_matches_oracle(qg, oracle, device):
     t = torch.empty(1 << 20, device=device)
     qg.fill_uniform(t, seed=9)
