@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-error-stats", action="store_true", help="skip the post-run quantization-error check")
     p.add_argument("--gather", action="store_true", help="also time the whole-node all-gather of C (N>1)")
     p.add_argument("--gemm-timing-every", type=int, default=5,
                    help="time the GEMM kernel on every n-th timed step (events cost ~4 us per timed step)")
@@ -267,6 +268,15 @@ def main():
     }
     if gather_ms is not None:
         result["allgather_C_ms"] = round(gather_ms, 3)
+    if rank == 0 and not args.no_error_stats:
+        # after the timed region: the quantization error of this run's output against the reference's
+        # unquantized op_mm (qgemm_mm_fp32, bit-exact sequential-k fmaf), computed on the device
+        C = qg.mm_fp32(X, W)
+        st = qg.error_stats(C, O, reference_order=M * N <= (1 << 24))
+        result["quant_error"] = {k: (None if v != v else float(f"{v:.6g}")) for k, v in st.items()}
+        result["quant_error"]["note"] = ("signed_mean_ref = the reference's printed metric (sequential fp32, "
+                                         "timing_quantize.cu:67-70); the others fp64 on the device")
+        del C
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(M, N, K, args.cpu_seconds)
     if rank == 0:

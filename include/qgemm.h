@@ -89,6 +89,16 @@ QGEMM_API int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride
                   const float *B, int64_t b_stride_h, int64_t b_stride_w,
                   float *C, int64_t c_stride_h, int64_t c_stride_w, int m, int n, int k, void *stream);
 
+/* The reference's quantization-error metric on the device: E = fl(C - O) per
+ * element (op_subtract, op_elemwise.cuh:531-542), C = the unquantized product, O = the quantized one;
+ * count elements, contiguous.  stats = DEVICE array of 5 doubles:
+ *   [0] the reference's "Mean Quantization error" (tensor.cuh:201-211: signed, summed sequentially in
+ *       fp32, / (float)count) -- computed only when reference_order != 0 (one lane, slow), else NaN
+ *   [1] signed mean (fp64)  [2] mean |E|  [3] max |E|  [4] mean |C|   (relative error = [2] / [4])
+ * Deterministic (fixed reduction tree for a given count). */
+QGEMM_API int qgemm_error_stats(const float *C, const float *O, int64_t count, int reference_order, double *stats,
+                      void *stream);
+
 /* Deterministic U[lo,hi) fill, bit-identical to oracle_fill_uniform (stands in for the
  * reference's cuRAND op_uniform_init, op_elemwise.cuh:728-744). */
 QGEMM_API int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, void *stream);

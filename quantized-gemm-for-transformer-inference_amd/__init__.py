@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "qgemm_mm_packed",
     "qgemm_mm_packed_i32",
     "qgemm_mm_fp32",
+    "qgemm_error_stats",
     "qgemm_set_gemm_events",
     "qgemm_set_event_mode",
     "qgemm_fill_uniform",
@@ -104,6 +105,8 @@ def load() -> ctypes.CDLL:
         L.qgemm_mm_packed_i32.restype = i32
         L.qgemm_mm_fp32.argtypes = [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, vp]
         L.qgemm_mm_fp32.restype = i32
+        L.qgemm_error_stats.argtypes = [vp, vp, i64, i32, vp, vp]
+        L.qgemm_error_stats.restype = i32
         L.qgemm_fill_uniform.argtypes = [vp, i64, ctypes.c_uint64, f32, f32, vp]
         L.qgemm_fill_uniform.restype = i32
         L.qgemm_set_gemm_events.argtypes = [vp, vp]
@@ -261,6 +264,24 @@ def mm_fp32(A, B, C=None):
                                                 B.stride(1), C.data_ptr(), C.stride(0), C.stride(1), M, N, K,
                                                 _stream(A.device)))
     return C
+
+
+def error_stats(C, O, reference_order: bool = False) -> dict:
+    """Quantization error of O against the unquantized C, on the device (qgemm_error_stats).
+
+    signed_mean_ref is the reference's printed metric (timing_quantize.cu:67-70 via tensor.cuh:201-211,
+    sequential fp32) -- only with reference_order=True (one GPU lane, slow at large sizes)."""
+    import torch
+    _require_device_f32(C, "C")
+    _require_device_f32(O, "O")
+    assert C.shape == O.shape and C.is_contiguous() and O.is_contiguous()
+    st = torch.empty(5, dtype=torch.float64, device=C.device)
+    _check("qgemm_error_stats", load().qgemm_error_stats(C.data_ptr(), O.data_ptr(), C.numel(),
+                                                        1 if reference_order else 0, st.data_ptr(),
+                                                        _stream(C.device)))
+    v = st.cpu().tolist()
+    return dict(signed_mean_ref=v[0], signed_mean=v[1], mean_abs=v[2], max_abs=v[3],
+                rel=v[2] / v[4] if v[4] else float("nan"))
 
 
 def fill_uniform(t, seed: int, lo: float = -1.0, hi: float = 1.0):

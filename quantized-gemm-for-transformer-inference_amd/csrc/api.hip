@@ -220,6 +220,16 @@ int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride_w, const 
                              static_cast<hipStream_t>(stream)));
 }
 
+int qgemm_error_stats(const float *C, const float *O, int64_t count, int reference_order, double *stats,
+                      void *stream) {
+    if (!C || !O || !stats || count < 1) return err(hipErrorInvalidValue);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    void *scratch = nullptr;
+    hipError_t e = cached_scratch(error_stats_scratch_bytes(), s, &scratch);
+    if (e != hipSuccess) return err(e);
+    return err(launch_error_stats(C, O, count, reference_order != 0, stats, scratch, s));
+}
+
 int qgemm_set_gemm_events(void *start_event, void *stop_event) {
     set_gemm_events(static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event));
     return 0;

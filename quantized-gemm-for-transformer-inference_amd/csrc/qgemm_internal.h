@@ -111,6 +111,10 @@ hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Ac
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
                          int64_t csh, int64_t csw, int m, int n, int k, hipStream_t stream);
 const char *gemm_config_name();
+// Quantization-error statistics on the device (error_stats.hip); scratch = error_stats_scratch_bytes().
+size_t error_stats_scratch_bytes();
+hipError_t launch_error_stats(const float *C, const float *O, int64_t n, bool reference_order, double *stats,
+                              void *scratch, hipStream_t stream);
 
 // Diagnostics: events to record exactly around the next GEMM kernel (hipExtLaunchKernelGGL), set
 // through qgemm_set_gemm_events() and consumed by one launch.  Thread-local.

@@ -185,6 +185,27 @@ def test_unquantized_gemm_matches_reference_order(qg, oracle, device):
         assert_bits_equal(C, oracle.mm_fp32(X, W), f"fp32 {M}x{N}x{K}")
 
 
+def test_device_error_stats_match_oracle(qg, oracle, device):
+    """the reference's error metric on the device.  The reference-order signed mean is
+    bit-identical to the sequential fp32 restatement; the fp64 statistics agree to rounding."""
+    M, N, K = 300, 257, 129
+    X, W = oracle.inputs(M, N, K, 81)
+    C_ref, O_ref = oracle.mm_fp32(X, W), oracle.quantized_mm(X, W)
+    want = oracle.error_stats(C_ref, O_ref)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    C = qg.mm_fp32(Xd, Wd)
+    O = torch.empty((M, N), device=device)
+    qg.op_quantized_mm(Xd, Wd, O, 127.0)
+    got = qg.error_stats(C, O, reference_order=True)
+    assert np.float32(got["signed_mean_ref"]).tobytes() == np.float32(want["signed_mean"]).tobytes()
+    for key in ("mean_abs", "max_abs", "rel"):
+        assert got[key] == pytest.approx(want[key], rel=1e-9, abs=0), key  # fp64 sums, different order
+    # fp64 signed mean vs the fp32 sequential one: same quantity, different rounding
+    assert got["signed_mean"] == pytest.approx(want["signed_mean"], rel=1e-3, abs=1e-7)
+    fast = qg.error_stats(C, O)
+    assert np.isnan(fast["signed_mean_ref"]) and fast["mean_abs"] == got["mean_abs"]
+
+
 def test_harness_binary_reproduces_reference_output(qg):
     import os
     import subprocess
