@@ -31,19 +31,20 @@ __device__ __forceinline__ float wave_max(float p) {
     return p;
 }
 
-__device__ __forceinline__ float cand_max(float p, float x) {
-    float a = absmax_candidate(x);
-    return (a > p) ? a : p;  // NaN never wins: comparison is false
-}
+// running max of |x| candidates; maxnum returns the non-NaN operand, so NaN never wins, exactly as
+// the reference's comparison (op_reduction.cuh:14-23) skips it
+__device__ __forceinline__ float cand_max(float p, float x) { return fmaxf(p, absmax_candidate(x)); }
 
 // partial encoding: candidates are >= +0 and NaN-free, so uint order of (bits + 1) is float order;
 // 0 means "no candidate in this chunk"
 __device__ __forceinline__ uint32_t enc_partial(float p) { return p >= 0.0f ? __float_as_uint(p) + 1u : 0u; }
 __device__ __forceinline__ float dec_partial(uint32_t e) { return e ? __uint_as_float(e - 1u) : -INFINITY; }
 
+// low bytes of a, b, c, d -> one dword (three v_perm_b32)
 __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
-    return (uint32_t)(a & 0xff) | ((uint32_t)(b & 0xff) << 8) | ((uint32_t)(c & 0xff) << 16) |
-           ((uint32_t)(d & 0xff) << 24);
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)d, (uint32_t)c, 0x0c0c0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
 // ------------------------------------------------------------------------------------------------

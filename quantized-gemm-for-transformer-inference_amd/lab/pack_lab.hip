@@ -8,9 +8,109 @@
 #include <functional>
 #include <cstring>
 
+#include <hip/hip_ext.h>
+
 #include "../csrc/pack.hip"
 
 using namespace qgemm;
+
+// ---- W-strip timeline probe: pack_w_strip_body's phases with s_memrealtime stamps (block-median) ----
+__device__ unsigned long long g_wst[4096][6];
+__global__ __launch_bounds__(1024) void wstrip_probe_kernel(const float *__restrict__ w, int64_t wsh, int k, int n,
+                                                            float range, float *__restrict__ scale,
+                                                            int8_t *__restrict__ q, int64_t k_pad, int nstrips) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
+    const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int c4 = t & 3, rq = t >> 2;
+    if (t == 0) g_wst[bid][0] = __builtin_amdgcn_s_memrealtime();
+    const int64_t n0 = (int64_t)strip * kWsCols;
+    float *red = reinterpret_cast<float *>(lds);
+    float *s_sh = red + 16 * 16;
+    uint8_t *img = lds + 4096;
+    const int64_t istride = k_pad + 16;
+    float4 v[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 1024 * i;
+            v[i][e] = (r < k) ? *reinterpret_cast<const float4 *>(w + (int64_t)r * wsh + n0 + 4 * c4)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 1024 * i;
+            if (r >= 1 && r < k) {
+                p0 = cand_max(p0, v[i][e].x);
+                p1 = cand_max(p1, v[i][e].y);
+                p2 = cand_max(p2, v[i][e].z);
+                p3 = cand_max(p3, v[i][e].w);
+            }
+        }
+    __syncthreads();
+    if (t == 0) g_wst[bid][1] = __builtin_amdgcn_s_memrealtime();  // all loads consumed
+#pragma unroll
+    for (int off = 4; off < 64; off <<= 1) {
+        p0 = fmaxf(p0, __shfl_xor(p0, off, 64));
+        p1 = fmaxf(p1, __shfl_xor(p1, off, 64));
+        p2 = fmaxf(p2, __shfl_xor(p2, off, 64));
+        p3 = fmaxf(p3, __shfl_xor(p3, off, 64));
+    }
+    if (lane < 4) {
+        red[wv * 16 + 4 * lane + 0] = p0;
+        red[wv * 16 + 4 * lane + 1] = p1;
+        red[wv * 16 + 4 * lane + 2] = p2;
+        red[wv * 16 + 4 * lane + 3] = p3;
+    }
+    __syncthreads();
+    if (t < kWsCols) {
+        float pp = red[t];
+#pragma unroll
+        for (int ww = 1; ww < 16; ++ww) pp = fmaxf(pp, red[ww * 16 + t]);
+        const float cw = absmax_finish(w[n0 + t], pp);
+        s_sh[t] = inv_divide(range, cw);
+        scale[n0 + t] = cw;
+    }
+    __syncthreads();
+    if (t == 0) g_wst[bid][2] = __builtin_amdgcn_s_memrealtime();  // scales known
+    const float s0 = s_sh[4 * c4 + 0], s1 = s_sh[4 * c4 + 1], s2 = s_sh[4 * c4 + 2], s3 = s_sh[4 * c4 + 3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r0 = 4 * rq + 1024 * i;
+        if (r0 >= k_pad) continue;
+        int qv[4][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool in = r0 + e < k;
+            qv[e][0] = in ? quant_i8(v[i][e].x, s0) : 0;
+            qv[e][1] = in ? quant_i8(v[i][e].y, s1) : 0;
+            qv[e][2] = in ? quant_i8(v[i][e].z, s2) : 0;
+            qv[e][3] = in ? quant_i8(v[i][e].w, s3) : 0;
+        }
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+            *reinterpret_cast<uint32_t *>(img + (int64_t)(4 * c4 + cc) * istride + r0) =
+                pack4(qv[0][cc], qv[1][cc], qv[2][cc], qv[3][cc]);
+    }
+    __syncthreads();
+    if (t == 0) g_wst[bid][3] = __builtin_amdgcn_s_memrealtime();  // image in LDS
+    const int64_t words = (int64_t)kWsCols * k_pad / 16;
+    for (int64_t x = t; x < words; x += 1024) {
+        const int64_t row = x / (k_pad / 16), col16 = x % (k_pad / 16);
+        *reinterpret_cast<uint4 *>(q + (n0 + row) * k_pad + col16 * 16) =
+            *reinterpret_cast<const uint4 *>(img + row * istride + col16 * 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) g_wst[bid][4] = __builtin_amdgcn_s_memrealtime();  // stores acknowledged
+}
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 int main(int argc, char **argv) {
@@ -41,13 +141,22 @@ int main(int argc, char **argv) {
         wonly(s1); xonly(s0);
         CK(hipEventRecord(join, s1)); CK(hipStreamWaitEvent(s0, join, 0));
     };
+    // same stream, the second kernel's dispatch packet without the barrier bit (hipExtAnyOrderLaunch):
+    // it may start while the first still runs; the next ordinary launch waits for both
+    auto x_any = [&](hipStream_t s) {
+        hipExtLaunchKernelGGL((pack_rows_vec_kernel<16>), dim3((unsigned)(vx2.rows_pad / 4)), dim3(256), 0, s, nullptr,
+                              nullptr, hipExtAnyOrderLaunch, (const float *)X, (int64_t)k, m, k, 127.f, vx2.scale,
+                              vx2.q, vx2.rows_pad, vx2.k_pad);
+        CK(hipGetLastError());
+    };
+    auto any_wx = [&]() { wonly(s0); x_any(s0); };
     auto wo = [&]() { wonly(s0); };
     auto xo = [&]() { xonly(s0); };
     struct V { const char *name; std::function<void()> f; };
     std::vector<V> vs = {{"single_pass", single}, {"w_then_x", seq}, {"concurrent", conc},
-                         {"concurrent_b", conc_xfirst}, {"w_only", wo}, {"x_only", xo}};
+                         {"concurrent_b", conc_xfirst}, {"anyorder_w_x", any_wx}, {"w_only", wo}, {"x_only", xo}};
     // parity: the split paths must give the same bytes as the single pass
-    single(); seq(); CK(hipStreamSynchronize(s0));
+    single(); any_wx(); CK(hipStreamSynchronize(s0));
     {
         size_t bx = packed_bytes(m, k), bw = packed_bytes(n, k);
         std::vector<char> a(bx), b(bx), c(bw), d(bw);
@@ -69,6 +178,27 @@ int main(int argc, char **argv) {
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             t[i].push_back(ms * 1000 / reps);
         }
+    {   // W-strip phase timeline (block-median, 100 MHz ticks -> us), after the timed rounds
+        const int nstrips = n / kWsCols;
+        const size_t lds = 4096 + (size_t)kWsCols * (vw2.k_pad + 16);
+        CK(hipFuncSetAttribute(reinterpret_cast<const void *>(wstrip_probe_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        for (int it = 0; it < 20; ++it)
+            wstrip_probe_kernel<<<nstrips, 1024, lds, s0>>>(W, n, k, n, 127.f, vw2.scale, vw2.q, vw2.k_pad, nstrips);
+        CK(hipStreamSynchronize(s0));
+        std::vector<unsigned long long> st((size_t)4096 * 6);
+        CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wst), st.size() * 8));
+        unsigned long long t0 = ~0ull;
+        for (int b = 0; b < nstrips; ++b) t0 = std::min(t0, st[(size_t)b * 6]);
+        const char *nm[5] = {"start", "loads consumed", "scales", "LDS image", "stores acked"};
+        for (int ph = 0; ph < 5; ++ph) {
+            std::vector<double> v;
+            for (int b = 0; b < nstrips; ++b) v.push_back((st[(size_t)b * 6 + ph] - t0) * 0.01);
+            std::sort(v.begin(), v.end());
+            printf("wstrip %-15s  min %6.2f  median %6.2f  max %6.2f us (from first block start)\n", nm[ph], v[0],
+                   v[v.size() / 2], v.back());
+        }
+    }
     const double bytes = 4.0 * m * k + 4.0 * k * n + (double)m * k + (double)k * n;
     for (size_t i = 0; i < vs.size(); ++i) {
         auto v = t[i]; std::sort(v.begin(), v.end());
