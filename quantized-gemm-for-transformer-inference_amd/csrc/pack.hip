@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
 // of 1024-thread blocks with two roles:
 //   W strip (blocks [0, n/16)): 16 columns x all K rows of W held in registers (16 float4 per
 //       thread), column absmax reduced on chip (shuffle + LDS), scales computed, quantized from the
-//       registers, transposed through a [16][k_pad] byte image in LDS, written as 16 packed rows.
+//       registers, stored as dwords of the 16 packed rows (4 k-bytes of one column each).
 //       W is read from HBM exactly once (the two-pass path reads it twice).
 //   X rows (remaining blocks): one wave per row, 16 rows per block (pack_rows_vec_body<16>).
 // Thread t of a W strip: c4 = t & 3 (columns n0 + 4*c4 .. +3), rq = t >> 2 (0..255): rows
@@ -358,8 +358,6 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
     const int64_t n0 = (int64_t)strip * kWsCols;
     float *red = reinterpret_cast<float *>(lds);                 // [16 waves][16 cols]
     float *s_sh = red + 16 * 16;                                 // [16] scales
-    uint8_t *img = lds + 4096;                                   // [16 rows][k_pad + 16 bytes]
-    const int64_t istride = k_pad + 16;                          // breaks the 4-way write conflict
     float4 v[4][4];                                              // [i][e]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -408,7 +406,9 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
     }
     __syncthreads();
     const float s0 = s_sh[4 * c4 + 0], s1 = s_sh[4 * c4 + 1], s2 = s_sh[4 * c4 + 2], s3 = s_sh[4 * c4 + 3];
-    // quantize; 4 consecutive rows of one column -> one dword of the transposed image
+    // quantize; 4 consecutive rows of one column = one dword of packed row n0+4c4+cc, stored directly:
+    // per wave instruction 4 runs of 64 B (16 rq lanes), the neighbouring waves complete each line in
+    // L2 (an LDS transpose to whole-row 16-B stores measured ~1 us slower per launch)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r0 = 4 * rq + 1024 * i;
@@ -424,16 +424,8 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
         }
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc)
-            *reinterpret_cast<uint32_t *>(img + (int64_t)(4 * c4 + cc) * istride + r0) =
+            *reinterpret_cast<uint32_t *>(q + (n0 + 4 * c4 + cc) * k_pad + r0) =
                 pack4(qv[0][cc], qv[1][cc], qv[2][cc], qv[3][cc]);
-    }
-    __syncthreads();
-    // write the 16 packed rows (k_pad bytes each) with 16-B stores
-    const int64_t words = (int64_t)kWsCols * k_pad / 16;
-    for (int64_t x = t; x < words; x += 1024) {
-        const int64_t row = x / (k_pad / 16), col16 = x % (k_pad / 16);
-        *reinterpret_cast<uint4 *>(q + (n0 + row) * k_pad + col16 * 16) =
-            *reinterpret_cast<const uint4 *>(img + row * istride + col16 * 16);
     }
 }
 
@@ -543,15 +535,7 @@ hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, Pa
     const int nstrips = n / kWsCols;
     const int npad = (int)((outw.rows_pad - n) / kWsCols);
     const int nx = (int)(outx.rows_pad / 16);
-    const size_t lds = 4096 + (size_t)kWsCols * (outx.k_pad + 16);
-    static bool attr_set = false;  // dynamic LDS above 64 KiB must be allowed explicitly
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(pack_single_pass_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           4096 + kWsCols * (kWsMaxK + 16));
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    const size_t lds = 4096;  // [16 waves][16 cols] partial maxima + 16 scales
     pack_single_pass_kernel<<<nstrips + npad + nx, 1024, lds, stream>>>(x, xsh, m, k, outx.scale, outx.q, outx.rows_pad,
                                                                          outx.k_pad, w, wsh, n, outw.scale, outw.q,
                                                                          outw.rows_pad, nstrips, range);
