@@ -434,6 +434,8 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
     int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    // roles by block id: [W strips][zero padding strips][X rows] (lab, 4096^3: 30.4 us; X rows first
+    // 31.5 us; W and X interleaved in groups of 8 blocks 35.1 us)
     const int bid = blockIdx.x;
     if (bid < nstrips) {
         // blocks b and b+8 run on one XCD: give them adjacent strips, so each 128-B line of W (two
