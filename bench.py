@@ -272,7 +272,7 @@ def main():
         # after the timed region: the quantization error of this run's output against the reference's
         # unquantized op_mm (qgemm_mm_fp32, bit-exact sequential-k fmaf), computed on the device
         C = qg.mm_fp32(X, W)
-        st = qg.error_stats(C, O, reference_order=M * N <= (1 << 24))
+        st = qg.error_stats(C, O, reference_order=M * N <= (1 << 24))  # sequential chain: ~tens of ms
         result["quant_error"] = {k: (None if v != v else float(f"{v:.6g}")) for k, v in st.items()}
         result["quant_error"]["note"] = ("signed_mean_ref = the reference's printed metric (sequential fp32, "
                                          "timing_quantize.cu:67-70); the others fp64 on the device")

@@ -4,7 +4,7 @@
 // op_subtract(C, qC, E) (op_elemwise.cuh:531-542, one fl(c - q) per element) then E.toHost().mean()
 // (tensor.cuh:201-211): a SIGNED sum accumulated sequentially in fp32 on the host, divided by
 // (float)(h*w).  At C4 sizes (M = 65536) the host round trip and the sequential sum dominate, so:
-//   stats[0]  the reference's number, same order and roundings (one lane walks the elements in order:
+//   stats[0]  the reference's number, same order and roundings (one wave walks the elements in order:
 //             exact, but latency-bound -- opt-in via reference_order)
 //   stats[1]  signed mean, fp64 accumulation (deterministic fixed-shape tree)
 //   stats[2]  mean |C - qC|   stats[3]  max |C - qC|   stats[4]  mean |C|  (relative = [2] / [4])
@@ -79,21 +79,43 @@ __global__ __launch_bounds__(kStatThreads) void error_final_kernel(const Acc4 *_
 }
 
 // tensor.cuh:201-211 on the host: float sum = 0; for each element sum += e; return sum / (h*w).
-// One lane, elements in order; loads run ahead in 16-element groups, the adds stay sequential.
-__global__ void error_reference_mean_kernel(const float *__restrict__ C, const float *__restrict__ O, int64_t n,
-                                            double *__restrict__ stats) {
-    if (threadIdx.x != 0) return;
+// One wave: chunk c+1 (1024 differences, coalesced) is loaded while chunk c, staged in LDS, is added
+// in element order -- the sum itself stays one sequential fp32 chain, as in the reference.
+constexpr int kRefChunk = 1024;
+__global__ __launch_bounds__(64) void error_reference_mean_kernel(const float *__restrict__ C,
+                                                                  const float *__restrict__ O, int64_t n,
+                                                                  double *__restrict__ stats) {
+    __shared__ float stage[2][kRefChunk];
+    const int lane = threadIdx.x;
+    auto fetch = [&](int64_t base, float (&d)[kRefChunk / 64]) {
+#pragma unroll
+        for (int j = 0; j < kRefChunk / 64; ++j) {
+            const int64_t i = base + j * 64 + lane;
+            d[j] = i < n ? __fsub_rn(C[i], O[i]) : 0.0f;
+        }
+    };
+    float d[kRefChunk / 64];
+    fetch(0, d);
     float sum = 0.0f;
-    int64_t i = 0;
-    for (; i + 16 <= n; i += 16) {
-        float d[16];
+    int buf = 0;
+    for (int64_t base = 0; base < n; base += kRefChunk, buf ^= 1) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) d[e] = __fsub_rn(C[i + e], O[i + e]);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) sum = __fadd_rn(sum, d[e]);
+        for (int j = 0; j < kRefChunk / 64; ++j) stage[buf][j * 64 + lane] = d[j];
+        __syncthreads();
+        if (base + kRefChunk < n) fetch(base + kRefChunk, d);  // in flight during the adds
+        const int cnt = n - base < kRefChunk ? (int)(n - base) : kRefChunk;
+        const float *sb = stage[buf];
+        int e = 0;
+        for (; e + 4 <= cnt; e += 4) {
+            const float4 q = *reinterpret_cast<const float4 *>(sb + e);  // same address in every lane
+            sum = __fadd_rn(sum, q.x);
+            sum = __fadd_rn(sum, q.y);
+            sum = __fadd_rn(sum, q.z);
+            sum = __fadd_rn(sum, q.w);
+        }
+        for (; e < cnt; ++e) sum = __fadd_rn(sum, sb[e]);
     }
-    for (; i < n; ++i) sum = __fadd_rn(sum, __fsub_rn(C[i], O[i]));
-    stats[0] = (double)__fdiv_rn(sum, (float)(int)n);  // h*w is an int in the reference
+    if (lane == 0) stats[0] = (double)__fdiv_rn(sum, (float)(int)n);  // h*w is an int in the reference
 }
 
 }  // namespace

@@ -2,12 +2,14 @@
 //
 // C[i,j] = dequant(sum_k A[i,k] * B[j,k]) with A = Xq [m_pad][k_pad], B = Wq^T [n_pad][k_pad] (packed,
 // k-contiguous, zero padded).  Macro-tile 256 x 256, k-step 128 bytes, 512 threads = 8 waves as
-// 2 (M) x 4 (N), each wave 128 x 64 = 4 x 2 tiles of v_mfma_i32_32x32x32_i8.
+// 2 (M) x 4 (N), each wave 128 x 64.  Product kernel: gemm_i8_v3 (8 x 4 tiles of
+// v_mfma_i32_16x16x64_i8 per wave, fused dequant epilogue, optional split-K); gemm_i8_v1 (4 x 2 tiles
+// of v_mfma_i32_32x32x32_i8) serves the raw int32 debug entry point.
 //
 // Staging: global_load_lds_dwordx4 (1 KiB per wave instruction = 8 rows x 128 B) into a 2-deep LDS
 // ring of 64 KiB stages; chunk g of LDS row r sits at slot g ^ ((r>>1)&7) (swizzle on the SOURCE
 // address; the LDS image stays lane-linear), which makes the fragment reads -- ds_read_b128 of one
-// 16-B chunk from 32 consecutive rows -- bank-conflict free.
+// 16-B chunk from 16 or 32 consecutive rows -- bank-conflict free.
 #pragma once
 
 #include "qgemm_internal.h"
