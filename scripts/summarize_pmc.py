@@ -18,7 +18,8 @@ from collections import defaultdict
 
 
 def short(name):
-    for key in ("gemm_i8", "pack_single_pass", "pack_rows_and_colmax", "pack_cols", "pack_rows", "colmax", "fill_uniform"):
+    for key in ("gemm_i8", "pack_single_pass", "pack_rows_and_colmax", "pack_cols", "pack_rows", "colmax",
+                "fill_uniform", "mm_f32", "error_partials", "error_final", "error_reference_mean"):
         if key in name:
             return key
     return name[-40:]
