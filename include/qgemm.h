@@ -89,6 +89,31 @@ QGEMM_API int qgemm_mm_fp32(const float *A, int64_t a_stride_h, int64_t a_stride
                   const float *B, int64_t b_stride_h, int64_t b_stride_w,
                   float *C, int64_t c_stride_h, int64_t c_stride_w, int m, int n, int k, void *stream);
 
+/* ---- The encoder counterpart (transformer.cu:14-77, BASELINE config 5) ----------
+ * Linear layer on the quantized path (linear.cuh:50-54): Y = quantized_mm(X, W) [+ b] [relu], where
+ * W (k x n) was packed once with qgemm_pack_b.  X is m x k row-major (row stride x_stride_h), Y m x n
+ * (row stride y_stride_h).  bias = NULL: no bias (relu requires a bias, as the reference's FFN).
+ * y = fl(O + b[j]) then (y < 0 ? 0 : y) (op_add, op_relu: op_elemwise.cuh:57-65, 181-195). */
+QGEMM_API size_t qgemm_linear_workspace_size(int m, int n, int k);
+QGEMM_API int qgemm_linear(const float *X, int64_t x_stride_h, int m, int k, const void *packed_w, int n,
+                 const float *bias, int relu, float *Y, int64_t y_stride_h, void *workspace, size_t ws_bytes,
+                 void *stream);
+/* op_multiply(S, scale) then op_softmax (attention.cuh:65-68, op_softmax.cuh:6-29), per row of w
+ * contiguous floats (w <= 4096); P may equal S.  exp is the correctly rounded fp32 exp. */
+QGEMM_API int qgemm_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, void *stream);
+/* op_add(A, B) then op_layernorm (transformer.cu:58-59, op_layernorm.cuh:6-33) as written:
+ * (y - mean) / var, sums in column order, pow(d, 2) = fl32(d*d); rows of w <= 4096 floats. */
+QGEMM_API int qgemm_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w, void *stream);
+/* Encoder stack with seeded weights drawn once and packed (the weight cache, s8f f2).  X, Y: seq x
+ * d_model row-major fp32 device arrays, seq <= max_seq <= 4096, d_model <= 4096, d_model % n_heads == 0.
+ * Weight tensor t of block i is the qgemm_fill_uniform stream encoder_weight_seed(seed, i, kind, head)
+ * = seed*1000003 + i*4099 + kind*131 + head, kind 0..7 = Wq, Wk, Wv, W_O, W1, b1, W2, b2, with the
+ * reference's init bounds (DESIGN.md "Encoder"). */
+QGEMM_API int qgemm_encoder_create(int d_model, int n_heads, int d_ff, int n_blocks, int max_seq, uint64_t seed,
+                         void **encoder);
+QGEMM_API int qgemm_encoder_forward(void *encoder, const float *X, float *Y, int seq, void *stream);
+QGEMM_API int qgemm_encoder_destroy(void *encoder);
+
 /* The reference's quantization-error metric on the device: E = fl(C - O) per
  * element (op_subtract, op_elemwise.cuh:531-542), C = the unquantized product, O = the quantized one;
  * count elements, contiguous.  stats = DEVICE array of 5 doubles:

@@ -66,6 +66,12 @@ def lib():
             L.oracle_signed_mean_error.argtypes = [_f32p, _f32p, _c_i64]
             L.oracle_error_stats.argtypes = [_f32p, _f32p, _c_i64, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+            L.oracle_softmax_rows.argtypes = [_f32p, _f32p, _c_i64, _c_int, _c_f]
+            L.oracle_add_layernorm_rows.argtypes = [_f32p, _f32p, _f32p, _c_i64, _c_int]
+            L.oracle_linear.argtypes = [_f32p, _f32p, ctypes.c_void_p, _c_int, _f32p, _c_int, _c_int, _c_int]
+            L.oracle_encoder_weight_seed.restype = _c_u64
+            L.oracle_encoder_weight_seed.argtypes = [_c_u64, _c_int, _c_int, _c_int]
+            L.oracle_encoder_forward.argtypes = [_f32p, _f32p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_u64]
             _lib = L
     return _lib
 
@@ -184,3 +190,46 @@ def error_stats(C, O) -> dict:
     lib().oracle_error_stats(C, O, C.size, ctypes.byref(a), ctypes.byref(m), ctypes.byref(r))
     return dict(signed_mean=signed_mean_error(C, O), mean_abs=a.value, max_abs=m.value,
                 rel=a.value / r.value if r.value else float("nan"))
+
+
+# ---- encoder counterpart (qgemm_oracle.c "Encoder counterpart") ----------------
+
+def softmax_rows(S, scale: float = 1.0):
+    """op_multiply(S, scale) + op_softmax per row (op_softmax.cuh:6-29), correctly rounded exp."""
+    S = _c(S, np.float32)
+    P = np.empty_like(S)
+    lib().oracle_softmax_rows(S, P, S.size // S.shape[-1], S.shape[-1], float(scale))
+    return P
+
+
+def add_layernorm_rows(A, B):
+    """op_add + op_layernorm as written (op_layernorm.cuh:6-33: (y - mean) / var)."""
+    A, B = _c(A, np.float32), _c(B, np.float32)
+    Y = np.empty_like(A)
+    lib().oracle_add_layernorm_rows(A, B, Y, A.size // A.shape[-1], A.shape[-1])
+    return Y
+
+
+def linear(X, W, b=None, relu=False):
+    """LinearLayer.forward with the quantized GEMM (linear.cuh:50-54) [+ op_relu]."""
+    X, W = _c(X, np.float32), _c(W, np.float32)
+    M, K = X.shape
+    N = W.shape[1]
+    Y = np.empty((M, N), np.float32)
+    bb = None if b is None else _c(b, np.float32)
+    lib().oracle_linear(X, W, None if bb is None else bb.ctypes.data, 1 if relu else 0, Y, M, N, K)
+    return Y
+
+
+def encoder_weight_seed(base: int, block: int, kind: int, head: int) -> int:
+    return int(lib().oracle_encoder_weight_seed(base, block, kind, head))
+
+
+def encoder_forward(X, d_model: int, n_heads: int, d_ff: int, n_blocks: int, seed: int):
+    """transformer.cu:14-77's Encoder with quantized linears (decisions: DESIGN.md "Encoder")."""
+    X = _c(X, np.float32)
+    seq = X.shape[0]
+    assert X.shape[1] == d_model
+    Y = np.empty_like(X)
+    lib().oracle_encoder_forward(X, Y, seq, d_model, n_heads, d_ff, n_blocks, seed)
+    return Y

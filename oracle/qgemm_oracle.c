@@ -331,3 +331,156 @@ void oracle_error_stats(const float *C, const float *O, int64_t n, double *mean_
     *max_abs = m;
     *mean_abs_ref = r / (double)n;
 }
+
+/* =================================================================================
+ * Encoder counterpart: transformer.cu:14-77 with the quantized linears,
+ * restated with the decisions documented in DESIGN.md "Encoder" (the reference's Encoder does
+ * not compile: arity at transformer.cu:37, ffnOut size at :62).
+ * ================================================================================= */
+
+/* op_mm<float,float> on strided views (Index(), tensor.cuh:14): res = +0, then fmaf over k
+ * ascending, then the zero products of the last 32-wide tile (op_mm.cuh:9-46). */
+static void mm_f32_strided(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw,
+                           float *C, int64_t csh, int64_t csw, int m, int n, int k)
+{
+    int kpad = ((k - 1) / ORACLE_TILE + 1) * ORACLE_TILE;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) {
+            float r = 0.0f;
+            for (int kk = 0; kk < k; ++kk) r = fmaf(A[i * ash + kk * asw], B[kk * bsh + j * bsw], r);
+            for (int kk = k; kk < kpad; ++kk) r = fmaf(0.0f, 0.0f, r);
+            C[i * csh + j * csw] = r;
+        }
+}
+
+/* op_multiply(S, scale) (attention.cuh:65) then op_softmax (op_softmax.cuh:6-29) per row:
+ * max seeded with the first element, strict '>'; exp as the correctly rounded fp32 exp
+ * fl32(exp((double)x)); sum in column order; divide. */
+void oracle_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < rows; ++r) {
+        const float *s = S + r * w;
+        float *p = P + r * w;
+        float mx = s[0] * scale;
+        for (int c = 1; c < w; ++c) {
+            float x = s[c] * scale;
+            if (x > mx) mx = x;
+        }
+        float sum = 0.0f;
+        for (int c = 0; c < w; ++c) {
+            float e = (float)exp((double)(s[c] * scale - mx));
+            p[c] = e;
+            sum += p[c];
+        }
+        for (int c = 0; c < w; ++c) p[c] = p[c] / sum;
+    }
+}
+
+/* op_add(A, B) (transformer.cu:58) then op_layernorm as written (op_layernorm.cuh:6-33):
+ * mean = sum/w, var = sum of pow(y-mean, 2) with CUDA's float pow(float,int) = fl(d*d), / w,
+ * out = (y - mean) / var. */
+void oracle_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < rows; ++r) {
+        const float *a = A + r * w, *b = B + r * w;
+        float *y = Y + r * w;
+        float mean = 0.0f, var = 0.0f;
+        for (int c = 0; c < w; ++c) mean += a[c] + b[c];
+        mean = mean / (float)w;
+        for (int c = 0; c < w; ++c) {
+            float d = (a[c] + b[c]) - mean;
+            var += d * d;
+        }
+        var = var / (float)w;
+        for (int c = 0; c < w; ++c) y[c] = ((a[c] + b[c]) - mean) / var;
+    }
+}
+
+/* LinearLayer.forward on the quantized path (linear.cuh:50-54, + op_relu): y = fl(O + b[j]),
+ * relu = (y < 0 ? 0 : y).  W is K x N row-major; b may be NULL. */
+void oracle_linear(const float *X, const float *W, const float *b, int relu, float *Y, int M, int N, int K)
+{
+    oracle_quantized_mm(X, W, Y, M, N, K, 127.0f);
+    if (!b) return;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < M; ++i)
+        for (int j = 0; j < N; ++j) {
+            float y = Y[(int64_t)i * N + j] + b[j];
+            if (relu && y < 0) y = 0;
+            Y[(int64_t)i * N + j] = y;
+        }
+}
+
+/* Seed of encoder weight tensor (block, kind, head), kind 0..7 = Wq Wk Wv Wo W1 b1 W2 b2
+ * (include/qgemm.h qgemm_encoder_create). */
+uint64_t oracle_encoder_weight_seed(uint64_t base, int block, int kind, int head)
+{
+    return base * 1000003ULL + (uint64_t)block * 4099ULL + (uint64_t)kind * 131ULL + (uint64_t)head;
+}
+
+/* "float max = 1.0f / std::sqrt(n)" with an int n (attention.cuh:38, linear.cuh:35) */
+static float init_bound(int n) { return (float)(1.0 / sqrt((double)n)); }
+
+void oracle_encoder_forward(const float *X, float *Y, int seq, int d, int H, int dff, int nblocks, uint64_t seed)
+{
+    const int dk = d / H;
+    const float scale = (float)(1.0 / sqrt((double)dk));
+    size_t S = (size_t)seq;
+    float *qkv = (float *)malloc(sizeof(float) * S * 3 * d);
+    float *scores = (float *)malloc(sizeof(float) * (size_t)H * S * S);
+    float *heads = (float *)malloc(sizeof(float) * S * d);
+    float *t = (float *)malloc(sizeof(float) * S * d);
+    float *x1 = (float *)malloc(sizeof(float) * S * d);
+    float *ffn = (float *)malloc(sizeof(float) * S * dff);
+    float *cur = (float *)malloc(sizeof(float) * S * d);
+    float *w = (float *)malloc(sizeof(float) * (size_t)(d > dff ? d : dff) * (size_t)(3 * d > dff ? 3 * d : dff));
+    float *one = (float *)malloc(sizeof(float) * (size_t)d * dk);
+    float *b = (float *)malloc(sizeof(float) * (size_t)(d > dff ? d : dff));
+    const float *in = X;
+    for (int i = 0; i < nblocks; ++i) {
+        float *out = (i == nblocks - 1) ? Y : cur;
+        /* [Wq | Wk | Wv], one d x dk tensor per (kind, head) (attention.cuh:37-41, :54-56) */
+        for (int kind = 0; kind < 3; ++kind)
+            for (int h = 0; h < H; ++h) {
+                float bd = init_bound(dk);
+                oracle_fill_uniform(one, (int64_t)d * dk, oracle_encoder_weight_seed(seed, i, kind, h), -bd, bd);
+                for (int r = 0; r < d; ++r)
+                    memcpy(w + (size_t)r * 3 * d + kind * d + h * dk, one + (size_t)r * dk, sizeof(float) * dk);
+            }
+        oracle_quantized_mm(in, w, qkv, seq, 3 * d, d, 127.0f);
+        for (int h = 0; h < H; ++h)   /* S_h = Q_h K_h^T (attention.cuh:58-60) */
+            mm_f32_strided(qkv + h * dk, 3 * d, 1, qkv + d + h * dk, 1, 3 * d, scores + (size_t)h * S * S, seq, 1,
+                           seq, seq, dk);
+        oracle_softmax_rows(scores, scores, (int64_t)H * seq, seq, scale);
+        for (int h = 0; h < H; ++h)   /* heads[:, h*dk..] = P_h V_h (attention.cuh:69, transformer.cu:43-50) */
+            mm_f32_strided(scores + (size_t)h * S * S, seq, 1, qkv + 2 * d + h * dk, 3 * d, 1, heads + h * dk, d, 1,
+                           seq, dk, seq);
+        /* output = multiHeadOut @ W_O (transformer.cu:52-54), W_O ~ U(-1, 1) */
+        oracle_fill_uniform(w, (int64_t)d * d, oracle_encoder_weight_seed(seed, i, 3, 0), -1.0f, 1.0f);
+        oracle_quantized_mm(heads, w, t, seq, d, d, 127.0f);
+        oracle_add_layernorm_rows(t, heads, x1, seq, d);   /* :58-59 */
+        /* FFN (transformer.cu:62-71, linear.cuh:34-39 bounds) */
+        float bd = init_bound(d), bf = init_bound(dff);
+        oracle_fill_uniform(w, (int64_t)d * dff, oracle_encoder_weight_seed(seed, i, 4, 0), -bd, bd);
+        oracle_fill_uniform(b, dff, oracle_encoder_weight_seed(seed, i, 5, 0), -bd, bd);
+        oracle_linear(x1, w, b, 1, ffn, seq, dff, d);
+        oracle_fill_uniform(w, (int64_t)dff * d, oracle_encoder_weight_seed(seed, i, 6, 0), -bf, bf);
+        oracle_fill_uniform(b, d, oracle_encoder_weight_seed(seed, i, 7, 0), -bf, bf);
+        oracle_linear(ffn, w, b, 0, t, seq, d, dff);
+        oracle_add_layernorm_rows(t, heads, out, seq, d);  /* :74-75 */
+        in = out;
+    }
+    free(qkv);
+    free(scores);
+    free(heads);
+    free(t);
+    free(x1);
+    free(ffn);
+    free(cur);
+    free(w);
+    free(one);
+    free(b);
+}

@@ -47,6 +47,13 @@ EXPORTED_SYMBOLS = (
     "qgemm_mm_packed_i32",
     "qgemm_mm_fp32",
     "qgemm_error_stats",
+    "qgemm_linear_workspace_size",
+    "qgemm_linear",
+    "qgemm_softmax_rows",
+    "qgemm_add_layernorm_rows",
+    "qgemm_encoder_create",
+    "qgemm_encoder_forward",
+    "qgemm_encoder_destroy",
     "qgemm_set_gemm_events",
     "qgemm_set_event_mode",
     "qgemm_fill_uniform",
@@ -107,6 +114,20 @@ def load() -> ctypes.CDLL:
         L.qgemm_mm_fp32.restype = i32
         L.qgemm_error_stats.argtypes = [vp, vp, i64, i32, vp, vp]
         L.qgemm_error_stats.restype = i32
+        L.qgemm_linear_workspace_size.argtypes = [i32, i32, i32]
+        L.qgemm_linear_workspace_size.restype = sz
+        L.qgemm_linear.argtypes = [vp, i64, i32, i32, vp, i32, vp, i32, vp, i64, vp, sz, vp]
+        L.qgemm_linear.restype = i32
+        L.qgemm_softmax_rows.argtypes = [vp, vp, i64, i32, f32, vp]
+        L.qgemm_softmax_rows.restype = i32
+        L.qgemm_add_layernorm_rows.argtypes = [vp, vp, vp, i64, i32, vp]
+        L.qgemm_add_layernorm_rows.restype = i32
+        L.qgemm_encoder_create.argtypes = [i32, i32, i32, i32, i32, ctypes.c_uint64, ctypes.POINTER(vp)]
+        L.qgemm_encoder_create.restype = i32
+        L.qgemm_encoder_forward.argtypes = [vp, vp, vp, i32, vp]
+        L.qgemm_encoder_forward.restype = i32
+        L.qgemm_encoder_destroy.argtypes = [vp]
+        L.qgemm_encoder_destroy.restype = i32
         L.qgemm_fill_uniform.argtypes = [vp, i64, ctypes.c_uint64, f32, f32, vp]
         L.qgemm_fill_uniform.restype = i32
         L.qgemm_set_gemm_events.argtypes = [vp, vp]
@@ -282,6 +303,90 @@ def error_stats(C, O, reference_order: bool = False) -> dict:
     v = st.cpu().tolist()
     return dict(signed_mean_ref=v[0], signed_mean=v[1], mean_abs=v[2], max_abs=v[3],
                 rel=v[2] / v[4] if v[4] else float("nan"))
+
+
+def linear(X, pw: Packed, bias=None, relu: bool = False, Y=None):
+    """LinearLayer.forward on the quantized path (linear.cuh:50-54): quantized_mm(X, W) [+ b] [relu],
+    W packed once by pack_b."""
+    import torch
+    _require_device_f32(X, "X")
+    assert X.stride(1) == 1 and X.shape[1] == pw.k
+    M, K = X.shape
+    N = pw.rows
+    if Y is None:
+        Y = torch.empty((M, N), dtype=torch.float32, device=X.device)
+    assert Y.shape == (M, N) and Y.stride(1) == 1
+    L = load()
+    ws = torch.empty(max(1, L.qgemm_linear_workspace_size(M, N, K)), dtype=torch.uint8, device=X.device)
+    b = 0 if bias is None else bias.data_ptr()
+    _check("qgemm_linear", L.qgemm_linear(X.data_ptr(), X.stride(0), M, K, pw.buf.data_ptr(), N, b, 1 if relu else 0,
+                                          Y.data_ptr(), Y.stride(0), ws.data_ptr(), ws.numel(), _stream(X.device)))
+    return Y
+
+
+def softmax_rows(S, scale: float = 1.0, P=None):
+    """op_multiply(S, scale) + op_softmax (attention.cuh:65-68) over the rows of a contiguous S."""
+    import torch
+    _require_device_f32(S, "S")
+    assert S.is_contiguous()
+    P = torch.empty_like(S) if P is None else P
+    _check("qgemm_softmax_rows", load().qgemm_softmax_rows(S.data_ptr(), P.data_ptr(), S.numel() // S.shape[-1],
+                                                          S.shape[-1], float(scale), _stream(S.device)))
+    return P
+
+
+def add_layernorm_rows(A, B, Y=None):
+    """op_add(A, B) + op_layernorm (transformer.cu:58-59, op_layernorm.cuh as written)."""
+    import torch
+    for t, nm in ((A, "A"), (B, "B")):
+        _require_device_f32(t, nm)
+        assert t.is_contiguous()
+    assert A.shape == B.shape
+    Y = torch.empty_like(A) if Y is None else Y
+    _check("qgemm_add_layernorm_rows", load().qgemm_add_layernorm_rows(A.data_ptr(), B.data_ptr(), Y.data_ptr(),
+                                                                      A.numel() // A.shape[-1], A.shape[-1],
+                                                                      _stream(A.device)))
+    return Y
+
+
+ENCODER_WEIGHT_KINDS = ("Wq", "Wk", "Wv", "Wo", "W1", "b1", "W2", "b2")
+
+
+def encoder_weight_seed(base: int, block: int, kind: int, head: int) -> int:
+    """Seed of one encoder weight tensor (include/qgemm.h, encoder.hip)."""
+    return (base * 1000003 + block * 4099 + kind * 131 + head) & 0xFFFFFFFFFFFFFFFF
+
+
+class Encoder:
+    """transformer.cu:14-77's Encoder with its linears on the quantized path."""
+
+    def __init__(self, d_model: int, n_heads: int, d_ff: int, n_blocks: int, max_seq: int, seed: int = 0):
+        self.d_model, self.n_heads, self.d_ff, self.n_blocks, self.max_seq, self.seed = (
+            d_model, n_heads, d_ff, n_blocks, max_seq, seed)
+        h = ctypes.c_void_p()
+        _check("qgemm_encoder_create", load().qgemm_encoder_create(d_model, n_heads, d_ff, n_blocks, max_seq, seed,
+                                                                  ctypes.byref(h)))
+        self._h = h
+
+    def forward(self, X, Y=None):
+        import torch
+        _require_device_f32(X, "X")
+        assert X.is_contiguous() and X.shape[1] == self.d_model
+        Y = torch.empty_like(X) if Y is None else Y
+        _check("qgemm_encoder_forward", load().qgemm_encoder_forward(self._h, X.data_ptr(), Y.data_ptr(), X.shape[0],
+                                                                    _stream(X.device)))
+        return Y
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().qgemm_encoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def fill_uniform(t, seed: int, lo: float = -1.0, hi: float = 1.0):

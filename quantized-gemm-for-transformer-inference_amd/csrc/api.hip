@@ -230,6 +230,57 @@ int qgemm_error_stats(const float *C, const float *O, int64_t count, int referen
     return err(launch_error_stats(C, O, count, reference_order != 0, stats, scratch, s));
 }
 
+int qgemm_linear(const float *X, int64_t x_stride_h, int m, int k, const void *packed_w, int n, const float *bias,
+                 int relu, float *Y, int64_t y_stride_h, void *workspace, size_t ws_bytes, void *stream) {
+    if (!X || !packed_w || !Y || m < 0 || n < 0 || k < 1 || (relu && !bias)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    const size_t need = qgemm_linear_workspace_size(m, n, k);
+    if (!workspace || ws_bytes < need) return err(hipErrorInvalidValue);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    char *scratch = static_cast<char *>(workspace);
+    const size_t sb = gemm_scratch_bytes(m, n, k);
+    char *pa = scratch + align256(sb);
+    const PackedView va = packed_view(pa, m, k);
+    hipError_t e = pack_vectors(X, x_stride_h, 1, m, k, kDefaultRange, va, s);
+    if (e != hipSuccess) return err(e);
+    const float inv_r2 = 1.0f / (kDefaultRange * kDefaultRange);
+    return err(launch_gemm_dequant(va, packed_view(packed_w, n, k), Y, y_stride_h, 1, m, n, inv_r2, scratch, sb, s, bias,
+                                   relu != 0));
+}
+
+size_t qgemm_linear_workspace_size(int m, int n, int k) {
+    if (m < 0 || n < 0 || k < 1) return 0;
+    return align256(gemm_scratch_bytes(m, n, k)) + align256(packed_bytes(m, k));
+}
+
+int qgemm_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, void *stream) {
+    if (!S || !P) return err(hipErrorInvalidValue);
+    return err(launch_softmax_rows(S, P, rows, w, scale, static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w, void *stream) {
+    if (!A || !B || !Y) return err(hipErrorInvalidValue);
+    return err(launch_add_layernorm_rows(A, B, Y, rows, w, static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_encoder_create(int d_model, int n_heads, int d_ff, int n_blocks, int max_seq, uint64_t seed,
+                         void **encoder) {
+    if (!encoder) return err(hipErrorInvalidValue);
+    Encoder *E = nullptr;
+    hipError_t e = encoder_create(d_model, n_heads, d_ff, n_blocks, max_seq, seed, &E);
+    *encoder = E;
+    return err(e);
+}
+
+int qgemm_encoder_forward(void *encoder, const float *X, float *Y, int seq, void *stream) {
+    return err(encoder_forward(static_cast<Encoder *>(encoder), X, Y, seq, static_cast<hipStream_t>(stream)));
+}
+
+int qgemm_encoder_destroy(void *encoder) {
+    encoder_destroy(static_cast<Encoder *>(encoder));
+    return 0;
+}
+
 int qgemm_set_gemm_events(void *start_event, void *stop_event) {
     set_gemm_events(static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event));
     return 0;

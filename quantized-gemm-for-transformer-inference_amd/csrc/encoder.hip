@@ -1,0 +1,212 @@
+// encoder.hip -- the encoder counterpart of the reference's transformer.cu:14-77 (SURVEY.md s8f f1,
+// BASELINE config 5) with its four GEMM call sites on the int8 quantized path:
+//   Q/K/V projections   attention.cuh:54-56   -> ONE quantized GEMM X @ [Wq | Wk | Wv] over all heads
+//                        (per-column absmax makes this bit-identical to per-head GEMMs)
+//   output projection    transformer.cu:52-54  -> quantized GEMM
+//   FFN linear 1 + relu  transformer.cu:64-66, linear.cuh:50-54 -> quantized GEMM, bias + relu fused
+//   FFN linear 2         transformer.cu:67-71  -> quantized GEMM, bias fused
+// QK^T and PV stay fp32 (activation x activation, attention.cuh:58-69): bit-exact op_mm<float>
+// (sequential-k fmaf), batched over heads.  Softmax and add + layernorm: encoder_ops.hip.
+//
+// Decisions where the reference cannot run as written ("Encoder"):
+//   * arity (transformer.cu:37 calls forward(X, X, out); attention.cuh:47 takes (X, out)): self
+//     attention on the block input;
+//   * d_ff (transformer.cu:62 sizes ffnOut {h, d_model}): the FFN hidden is {seq, d_ff};
+//   * weights are drawn ONCE per encoder (the reference re-draws them on every call, :34, :53, :63):
+//     they are packed once (the LLM.int8() weight cache, s8f f2) -- seeded, reproducible;
+//   * heads are written straight into their column slice of multiHeadOut (no host round trip,
+//     :43-50); the residual adds multiHeadOut, as the reference does (:58, :74).
+#include <cmath>
+#include <new>
+#include <vector>
+
+#include "qgemm_internal.h"
+
+namespace qgemm {
+
+namespace {
+
+enum WeightKind { kWq = 0, kWk = 1, kWv = 2, kWo = 3, kW1 = 4, kB1 = 5, kW2 = 6, kB2 = 7 };
+
+}  // namespace
+
+// Seed of one weight tensor: every tensor its own counter stream (documented for the oracle).
+uint64_t encoder_weight_seed(uint64_t base, int block, int kind, int head) {
+    return base * 1000003ULL + (uint64_t)block * 4099ULL + (uint64_t)kind * 131ULL + (uint64_t)head;
+}
+
+// fl32(1 / sqrt(n)): the reference's "float max = 1.0f / std::sqrt(n)" with an int n (double sqrt).
+float encoder_init_bound(int n) { return (float)(1.0 / std::sqrt((double)n)); }
+
+struct EncoderBlock {
+    void *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;  // packed (W^T int8 + Cw)
+    float *b1 = nullptr, *b2 = nullptr;
+};
+
+struct Encoder {
+    int d_model = 0, n_heads = 0, d_ff = 0, n_blocks = 0, max_seq = 0;
+    std::vector<EncoderBlock> blocks;
+    float *qkv = nullptr, *scores = nullptr, *heads = nullptr, *t = nullptr, *ffn = nullptr, *x1 = nullptr;
+    float *xa = nullptr, *xb = nullptr;
+    char *ws = nullptr;  // [split-K scratch][packed activations]
+    size_t scratch_bytes = 0, ws_bytes = 0;
+};
+
+namespace {
+
+hipError_t alloc(void **p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 16); }
+
+template <typename T>
+hipError_t alloc_f(T **p, size_t count) {
+    return alloc(reinterpret_cast<void **>(p), count * sizeof(T));
+}
+
+// draw a K x N fp32 weight (uniform [-bound, bound), reference init formula) and pack it as B
+hipError_t make_packed(int k, int n, const std::vector<uint64_t> &col_seeds, int cols_per_seed, float bound,
+                       void **packed, float *tmp, hipStream_t s) {
+    // col_seeds[c] fills columns [c*cols_per_seed, (c+1)*cols_per_seed) -- one reference tensor each
+    hipError_t e;
+    float *one = tmp + (size_t)k * n;  // k x cols_per_seed staging
+    for (size_t c = 0; c < col_seeds.size(); ++c) {
+        if ((e = launch_fill_uniform(one, (int64_t)k * cols_per_seed, col_seeds[c], -bound, bound, s)) != hipSuccess)
+            return e;
+        if ((e = hipMemcpy2DAsync(tmp + c * cols_per_seed, sizeof(float) * n, one, sizeof(float) * cols_per_seed,
+                                  sizeof(float) * cols_per_seed, k, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return e;
+    }
+    if ((e = alloc(packed, packed_bytes(n, k))) != hipSuccess) return e;
+    // B = W (k x n, row-major): reduction vectors are its columns -> pack_cols path
+    return launch_pack_cols(tmp, n, k, n, 127.0f, packed_view(*packed, n, k), s);
+}
+
+hipError_t linear(Encoder &E, const float *x, int seq, int k, const void *wpacked, int n, float *y,
+                  const float *bias, bool relu, hipStream_t s) {
+    // pack the activations (Cx per row: op_absmax(X), X_int8), then the GEMM with the fused epilogue
+    char *pa = E.ws + E.scratch_bytes;
+    const PackedView va = packed_view(pa, seq, k);
+    hipError_t e = launch_pack_rows(x, k, 1, seq, k, 127.0f, va, s);
+    if (e != hipSuccess) return e;
+    const float inv_r2 = 1.0f / (127.0f * 127.0f);
+    return launch_gemm_dequant(va, packed_view(wpacked, n, k), y, n, 1, seq, n, inv_r2, E.ws, E.scratch_bytes, s,
+                               bias, relu);
+}
+
+}  // namespace
+
+void encoder_destroy(Encoder *E) {
+    if (!E) return;
+    for (auto &b : E->blocks) {
+        (void)hipFree(b.wqkv);
+        (void)hipFree(b.wo);
+        (void)hipFree(b.w1);
+        (void)hipFree(b.w2);
+        (void)hipFree(b.b1);
+        (void)hipFree(b.b2);
+    }
+    for (void *p : {(void *)E->qkv, (void *)E->scores, (void *)E->heads, (void *)E->t, (void *)E->ffn, (void *)E->x1,
+                    (void *)E->xa, (void *)E->xb, (void *)E->ws})
+        (void)hipFree(p);
+    delete E;
+}
+
+hipError_t encoder_create(int d_model, int n_heads, int d_ff, int n_blocks, int max_seq, uint64_t seed,
+                          Encoder **out) {
+    *out = nullptr;
+    if (d_model < 2 || n_heads < 1 || d_model % n_heads || d_ff < 2 || n_blocks < 1 || max_seq < 1 ||
+        max_seq > 4096 || d_model > 4096)
+        return hipErrorInvalidValue;
+    Encoder *E = new (std::nothrow) Encoder;
+    if (!E) return hipErrorOutOfMemory;
+    E->d_model = d_model;
+    E->n_heads = n_heads;
+    E->d_ff = d_ff;
+    E->n_blocks = n_blocks;
+    E->max_seq = max_seq;
+    E->blocks.resize(n_blocks);
+    const int d = d_model, dk = d_model / n_heads;
+    const size_t S = (size_t)max_seq;
+    hipError_t e = hipSuccess;
+    auto fail = [&](hipError_t err) {
+        encoder_destroy(E);
+        return err;
+    };
+    if ((e = alloc_f(&E->qkv, S * 3 * d)) || (e = alloc_f(&E->scores, (size_t)n_heads * S * S)) ||
+        (e = alloc_f(&E->heads, S * d)) || (e = alloc_f(&E->t, S * d)) || (e = alloc_f(&E->ffn, S * d_ff)) ||
+        (e = alloc_f(&E->x1, S * d)) || (e = alloc_f(&E->xa, S * d)) || (e = alloc_f(&E->xb, S * d)))
+        return fail(e);
+    // workspace: split-K scratch for the largest of the four linear shapes + packed activations
+    const int shapes[4][2] = {{3 * d, d}, {d, d}, {d_ff, d}, {d, d_ff}};  // (n, k)
+    size_t scratch = 0, act = 0;
+    for (auto &sh : shapes) {
+        scratch = std::max(scratch, gemm_scratch_bytes(max_seq, sh[0], sh[1]));
+        act = std::max(act, packed_bytes(max_seq, sh[1]));
+    }
+    E->scratch_bytes = (scratch + 255) & ~(size_t)255;
+    E->ws_bytes = E->scratch_bytes + act;
+    if ((e = alloc(reinterpret_cast<void **>(&E->ws), E->ws_bytes))) return fail(e);
+
+    // weights, drawn once with the reference's init bounds (attention.cuh:37-41, linear.cuh:34-39,
+    // transformer.cu:53) and packed
+    const size_t maxk = std::max(d, d_ff), maxn = std::max(3 * d, d_ff);
+    float *tmp = nullptr;
+    if ((e = alloc_f(&tmp, maxk * maxn + maxk * maxn))) return fail(e);
+    hipStream_t s = nullptr;
+    for (int i = 0; i < n_blocks && e == hipSuccess; ++i) {
+        EncoderBlock &B = E->blocks[i];
+        std::vector<uint64_t> qkv_seeds;
+        for (int kind = kWq; kind <= kWv; ++kind)
+            for (int h = 0; h < n_heads; ++h) qkv_seeds.push_back(encoder_weight_seed(seed, i, kind, h));
+        if ((e = make_packed(d, 3 * d, qkv_seeds, dk, encoder_init_bound(dk), &B.wqkv, tmp, s))) break;
+        if ((e = make_packed(d, d, {encoder_weight_seed(seed, i, kWo, 0)}, d, 1.0f, &B.wo, tmp, s))) break;
+        if ((e = make_packed(d, d_ff, {encoder_weight_seed(seed, i, kW1, 0)}, d_ff, encoder_init_bound(d), &B.w1, tmp,
+                             s)))
+            break;
+        if ((e = make_packed(d_ff, d, {encoder_weight_seed(seed, i, kW2, 0)}, d, encoder_init_bound(d_ff), &B.w2, tmp,
+                             s)))
+            break;
+        if ((e = alloc_f(&B.b1, d_ff)) || (e = alloc_f(&B.b2, d))) break;
+        const float bd = encoder_init_bound(d), bf = encoder_init_bound(d_ff);
+        if ((e = launch_fill_uniform(B.b1, d_ff, encoder_weight_seed(seed, i, kB1, 0), -bd, bd, s))) break;
+        if ((e = launch_fill_uniform(B.b2, d, encoder_weight_seed(seed, i, kB2, 0), -bf, bf, s))) break;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return fail(e);
+    *out = E;
+    return hipSuccess;
+}
+
+hipError_t encoder_forward(Encoder *E, const float *X, float *Y, int seq, hipStream_t s) {
+    if (!E || !X || !Y || seq < 1 || seq > E->max_seq) return hipErrorInvalidValue;
+    const int d = E->d_model, H = E->n_heads, dk = d / H;
+    const float scale = (float)(1.0 / std::sqrt((double)dk));  // attention.cuh:64
+    const float *in = X;
+    hipError_t e;
+    for (int i = 0; i < E->n_blocks; ++i) {
+        const EncoderBlock &B = E->blocks[i];
+        float *out = (i == E->n_blocks - 1) ? Y : (i % 2 ? E->xb : E->xa);
+        // [Q | K | V] = X @ [Wq | Wk | Wv]                              (attention.cuh:54-56, all heads)
+        if ((e = linear(*E, in, seq, d, B.wqkv, 3 * d, E->qkv, nullptr, false, s))) return e;
+        // S_h = Q_h K_h^T, fp32 op_mm with the transposed view           (attention.cuh:58-60)
+        if ((e = launch_mm_f32_batched(E->qkv, 3 * d, 1, dk, E->qkv + d, 1, 3 * d, dk, E->scores, seq, 1,
+                                       (int64_t)seq * seq, seq, seq, dk, H, s)))
+            return e;
+        // P_h = softmax(S_h * 1/sqrt(d_k)), in place                     (attention.cuh:65-68)
+        if ((e = launch_softmax_rows(E->scores, E->scores, (int64_t)H * seq, seq, scale, s))) return e;
+        // heads[:, h*d_v..] = P_h V_h                                    (attention.cuh:69, transformer.cu:43-50)
+        if ((e = launch_mm_f32_batched(E->scores, seq, 1, (int64_t)seq * seq, E->qkv + 2 * d, 3 * d, 1, dk, E->heads,
+                                       d, 1, dk, seq, dk, seq, H, s)))
+            return e;
+        // output = multiHeadOut @ W_O; LN(output + multiHeadOut)         (transformer.cu:52-59)
+        if ((e = linear(*E, E->heads, seq, d, B.wo, d, E->t, nullptr, false, s))) return e;
+        if ((e = launch_add_layernorm_rows(E->t, E->heads, E->x1, seq, d, s))) return e;
+        // FFN: relu(x1 W1 + b1) W2 + b2; LN(ffn + multiHeadOut)          (transformer.cu:62-75)
+        if ((e = linear(*E, E->x1, seq, d, B.w1, E->d_ff, E->ffn, B.b1, true, s))) return e;
+        if ((e = linear(*E, E->ffn, seq, E->d_ff, B.w2, d, E->t, B.b2, false, s))) return e;
+        if ((e = launch_add_layernorm_rows(E->t, E->heads, out, seq, d, s))) return e;
+        in = out;
+    }
+    return hipSuccess;
+}
+
+}  // namespace qgemm

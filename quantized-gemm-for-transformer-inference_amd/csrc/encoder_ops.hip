@@ -1,0 +1,125 @@
+// encoder_ops.hip -- the row operations of the encoder counterpart that sit
+// between its quantized linears: the reference's op_multiply + op_softmax (attention.cuh:65-68,
+// op_softmax.cuh:6-29) and op_add + op_layernorm (transformer.cu:58-59, op_layernorm.cuh:6-33).
+//
+// The reference runs one THREAD per row with sequential fp32 sums.  Here one WAVE per row: the
+// elementwise parts run across the lanes, and each sum stays ONE sequential fp32 chain in element
+// order (the row is staged in LDS and every lane walks it), so the results keep the reference's
+// rounding sequence.  Decisions where the reference is not defined precisely (encoder):
+//   exp    : correctly rounded fp32 exp, fl32(exp((double)x)) (CUDA's expf is within 2 ulp, host
+//            expf differs again; the oracle uses the same definition)
+//   pow(d,2): fl32(d * d) (CUDA's float pow(float, int) overload)
+//   grids  : every row is processed (the reference's launch covers ceil(w/256)*256 rows, which is
+//            all of them whenever w >= h, as in every shape it runs)
+#include "qgemm_internal.h"
+
+namespace qgemm {
+
+namespace {
+
+constexpr int kRowWaves = 4;       // rows per 256-thread block
+constexpr int kMaxRowLen = 4096;   // LDS staging per wave: 16 KiB
+
+// sequential fp32 sum of row[0..w) in element order (every lane computes the same chain)
+__device__ __forceinline__ float seq_sum(const float *row, int w) {
+    float sum = 0.0f;
+    int e = 0;
+    for (; e + 16 <= w; e += 16) {
+        float4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(row + e + 4 * j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sum = __fadd_rn(sum, q[j].x);
+            sum = __fadd_rn(sum, q[j].y);
+            sum = __fadd_rn(sum, q[j].z);
+            sum = __fadd_rn(sum, q[j].w);
+        }
+    }
+    for (; e < w; ++e) sum = __fadd_rn(sum, row[e]);
+    return sum;
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) void softmax_rows_kernel(const float *S, float *P, int64_t rows, int w,
+                                                                      float scale) {  // P may be S (in place)
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
+    if (row >= rows) return;
+    const float *s = S + row * w;
+    float *p = P + row * w;
+    float *st = stage + wv * ((w + 3) & ~3);  // 16-B aligned row stage
+    // max: seed = first element, then "if (x > max) max = x" (op_softmax.cuh:13-18) -- NaN never wins
+    const float seed = __fmul_rn(s[0], scale);
+    float cand = -INFINITY;
+    for (int c = lane + 1; c < w; c += 64) {
+        const float x = __fmul_rn(s[c], scale);  // op_multiply(QK_T, scale_factor) (attention.cuh:65)
+        cand = (x > cand) ? x : cand;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(cand, off, 64);
+        cand = (o > cand) ? o : cand;
+    }
+    const float mx = (cand > seed) ? cand : seed;
+    for (int c = lane; c < w; c += 64) {
+        const float d = __fsub_rn(__fmul_rn(s[c], scale), mx);
+        st[c] = (float)exp((double)d);  // correctly rounded fp32 exp
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done (one wave per row)
+    __builtin_amdgcn_wave_barrier();
+    const float sum = seq_sum(st, w);   // op_softmax.cuh:20-24, in column order
+    for (int c = lane; c < w; c += 64) p[c] = __fdiv_rn(st[c], sum);
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(const float *__restrict__ A,
+                                                                            const float *__restrict__ B,
+                                                                            float *__restrict__ Y, int64_t rows,
+                                                                            int w) {
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
+    if (row >= rows) return;
+    const float *a = A + row * w, *b = B + row * w;
+    float *y = Y + row * w;
+    float *st = stage + wv * ((w + 3) & ~3);
+    for (int c = lane; c < w; c += 64) st[c] = __fadd_rn(a[c], b[c]);  // op_add (transformer.cu:58)
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const float fw = (float)w;                                 // "mean/w": int -> float
+    const float mean = __fdiv_rn(seq_sum(st, w), fw);          // op_layernorm.cuh:15-19
+    __builtin_amdgcn_wave_barrier();
+    // the squared deviations replace the row in LDS (each lane rewrites the columns it owns)
+    for (int c = lane; c < w; c += 64) {
+        const float d = __fsub_rn(st[c], mean);
+        st[c] = __fmul_rn(d, d);                               // pow(x - mean, 2) as fp32 d*d
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const float var = __fdiv_rn(seq_sum(st, w), fw);           // :21-25
+    for (int c = lane; c < w; c += 64)                         // (x - mean) / var (:28), as written
+        y[c] = __fdiv_rn(__fsub_rn(__fadd_rn(a[c], b[c]), mean), var);
+}
+
+}  // namespace
+
+hipError_t launch_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, hipStream_t stream) {
+    if (w < 1 || w > kMaxRowLen || rows < 0) return hipErrorInvalidValue;
+    if (rows == 0) return hipSuccess;
+    const size_t lds = sizeof(float) * kRowWaves * ((w + 3) & ~3);
+    softmax_rows_kernel<<<(unsigned)((rows + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds, stream>>>(S, P, rows, w,
+                                                                                                      scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w,
+                                     hipStream_t stream) {
+    if (w < 1 || w > kMaxRowLen || rows < 0) return hipErrorInvalidValue;
+    if (rows == 0) return hipSuccess;
+    const size_t lds = sizeof(float) * kRowWaves * ((w + 3) & ~3);
+    add_layernorm_rows_kernel<<<(unsigned)((rows + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds, stream>>>(
+        A, B, Y, rows, w);
+    return hipGetLastError();
+}
+
+}  // namespace qgemm

@@ -17,7 +17,11 @@ constexpr int TM = 64, TN = 64, TK = 16;
 __global__ __launch_bounds__(256) void mm_f32_kernel(const float *__restrict__ A, int64_t ash, int64_t asw,
                                                      const float *__restrict__ B, int64_t bsh, int64_t bsw,
                                                      float *__restrict__ C, int64_t csh, int64_t csw, int m, int n,
-                                                     int k) {
+                                                     int k, int64_t a_bs, int64_t b_bs, int64_t c_bs) {
+    // batch z (attention heads): operands offset by the batch strides
+    A += blockIdx.z * a_bs;
+    B += blockIdx.z * b_bs;
+    C += blockIdx.z * c_bs;
     __shared__ float As[TK][TM + 1];
     __shared__ float Bs[TK][TN + 1];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -65,8 +69,14 @@ __global__ __launch_bounds__(256) void mm_f32_kernel(const float *__restrict__ A
 
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
                          int64_t csh, int64_t csw, int m, int n, int k, hipStream_t stream) {
-    const dim3 grid((unsigned)((n + TN - 1) / TN), (unsigned)((m + TM - 1) / TM));
-    mm_f32_kernel<<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k);
+    return launch_mm_f32_batched(A, ash, asw, 0, B, bsh, bsw, 0, C, csh, csw, 0, m, n, k, 1, stream);
+}
+
+hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64_t a_bs, const float *B, int64_t bsh,
+                                 int64_t bsw, int64_t b_bs, float *C, int64_t csh, int64_t csw, int64_t c_bs, int m,
+                                 int n, int k, int batch, hipStream_t stream) {
+    const dim3 grid((unsigned)((n + TN - 1) / TN), (unsigned)((m + TM - 1) / TM), (unsigned)batch);
+    mm_f32_kernel<<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs, c_bs);
     return hipGetLastError();
 }
 

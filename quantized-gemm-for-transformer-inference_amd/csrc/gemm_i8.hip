@@ -51,11 +51,27 @@ size_t gemm_scratch_bytes(int m, int n, int k) {
     return ticket_bytes(tiles) + (size_t)tiles * s * kSlabInts * 4;
 }
 
+template <int kEpi>
+static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
+    const GemmEvents ev = take_gemm_events();
+    if ((ev.start || ev.stop) && g_event_mode == 0) {
+        hipExtLaunchKernelGGL((gemm_i8_v3<kStoreLds, true, kPrio, kEpi>), grid, dim3(kThreads), 0, stream, ev.start,
+                              ev.stop, 0, p);
+        return hipGetLastError();
+    }
+    if (ev.start) (void)hipEventRecord(ev.start, stream);
+    gemm_i8_v3<kStoreLds, true, kPrio, kEpi><<<grid, dim3(kThreads), 0, stream>>>(p);
+    hipError_t e = hipGetLastError();
+    if (ev.stop) (void)hipEventRecord(ev.stop, stream);
+    return e;
+}
+
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw, int m,
-                               int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+                               int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
+                               const float *bias, bool relu) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
-               inv_r2, 1, nullptr, nullptr};
+               inv_r2, 1, nullptr, nullptr, bias};
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
     const int splits = gemm_splits(m, n, (int)a.k_pad);
     if (splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
@@ -67,23 +83,14 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
         if (e != hipSuccess) return e;
     }
     const dim3 grid((unsigned)(tiles * p.splits));
-    const GemmEvents ev = take_gemm_events();
-    if ((ev.start || ev.stop) && g_event_mode == 0) {
-        hipExtLaunchKernelGGL((gemm_i8_v3<kStoreLds, true, kPrio>), grid, dim3(kThreads), 0, stream, ev.start, ev.stop,
-                              0, p);
-        return hipGetLastError();
-    }
-    if (ev.start) (void)hipEventRecord(ev.start, stream);
-    gemm_i8_v3<kStoreLds, true, kPrio><<<grid, dim3(kThreads), 0, stream>>>(p);
-    hipError_t e = hipGetLastError();
-    if (ev.stop) (void)hipEventRecord(ev.stop, stream);
-    return e;
+    if (!bias) return launch_v3<kEpiNone>(p, grid, stream);
+    return relu ? launch_v3<kEpiBiasRelu>(p, grid, stream) : launch_v3<kEpiBias>(p, grid, stream);
 }
 
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n, hipStream_t stream) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, Acc, n, 1, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
-               0.0f, 1, nullptr, nullptr};
+               0.0f, 1, nullptr, nullptr, nullptr};
     gemm_i8_v1<kStoreDirect, false><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
     return hipGetLastError();
 }

@@ -71,7 +71,12 @@ struct GemmArgs {
     int splits;
     int32_t *slabs;     // tiles x splits x (BM x BN) int32, MFMA-native order
     unsigned *tickets;  // tiles words, zeroed before every launch
+    const float *bias;  // n floats, added after the dequantize (kEpi >= 1)
 };
+
+// Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
+// y = fl(O + b[j]) then relu(y) = (y < 0 ? 0 : y) -- each its own rounding, as the separate launches.
+enum EpiMode { kEpiNone = 0, kEpiBias = 1, kEpiBiasRelu = 2 };
 
 constexpr int64_t kSlabInts = (int64_t)BM * BN;
 
@@ -278,7 +283,14 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v1(GemmArgs p) {
 //                  128 KiB staging ring + 2 KiB for the scales.
 //   kStoreDirect : one dword per lane per register (4 rows x 64 B per instruction).
 //   kStoreNone   : ablation -- keep the accumulators live, store nothing.
-template <int kMode>
+template <int kEpi>
+__device__ __forceinline__ float epi_extra(float o, const float *sB, int jl) {
+    if constexpr (kEpi >= kEpiBias) o = __fadd_rn(o, sB[jl]);
+    if constexpr (kEpi == kEpiBiasRelu) o = (o < 0.0f) ? 0.0f : o;
+    return o;
+}
+
+template <int kMode, int kEpi = kEpiNone>
 __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (&acc)[8][4], int tm, int tn, int wm,
                                            int wn, int lane, int tid) {
     const int gi0 = tm * BM, gj0 = tn * BN;
@@ -296,10 +308,13 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
     }
     float *sCx = reinterpret_cast<float *>(lds + kLdsBytes);
     float *sCw = sCx + BM;
+    float *sB = sCw + BN;  // bias (kEpi >= 1): needs kLdsBytes + 3 KiB
     float *C = static_cast<float *>(p.C);
     __syncthreads();  // every wave is done with the staging ring
     if (tid < BM) sCx[tid] = p.Cx[gi0 + tid];
     else sCw[tid - BM] = p.Cw[gj0 + tid - BM];
+    if constexpr (kEpi >= kEpiBias)
+        if (tid < BN) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
     if constexpr (kMode == kStoreDirect) {
         __syncthreads();
 #pragma unroll
@@ -313,7 +328,8 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
                 for (int r = 0; r < 4; ++r) {
                     const int il = wm * 128 + mi * 16 + 4 * kq + r;
                     const int i = gi0 + il;
-                    const float o = dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2);
+                    const float o =
+                        epi_extra<kEpi>(dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2), sB, jl);
                     if (i < p.m && j < p.n) C[(int64_t)i * p.csh + (int64_t)j * p.csw] = o;
                 }
         }
@@ -334,8 +350,8 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int il = mi * 16 + 4 * kq + r;
-                            T[il * BN + jl] =
-                                dequantize(acc[mi][ni][r], outer_product(sCx[half * 128 + il], cw), p.inv_r2);
+                            T[il * BN + jl] = epi_extra<kEpi>(
+                                dequantize(acc[mi][ni][r], outer_product(sCx[half * 128 + il], cw), p.inv_r2), sB, jl);
                         }
                 }
             }
@@ -405,9 +421,10 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, int8_t *lds, v
     return true;
 }
 
-template <int kMode, bool kDequant, int kFlags = 0>
+template <int kMode, bool kDequant, int kFlags = 0, int kEpi = kEpiNone>
 __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
-    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + 2048];  // + scales for the epilogue
+    // + scales (and bias) for the epilogue
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + (kEpi >= kEpiBias ? 3072 : 2048)];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -473,7 +490,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
     }
 
     if (S > 1 && !splitk_combine(p, lds, acc, tile, slice, S, wave, lane, tid)) return;
-    epilogue16<kMode>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+    epilogue16<kMode, kEpi>(p, lds, acc, tm, tn, wm, wn, lane, tid);
 }
 
 

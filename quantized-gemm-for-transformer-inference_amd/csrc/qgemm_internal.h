@@ -106,12 +106,30 @@ hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float l
 int gemm_splits(int m, int n, int k);
 size_t gemm_scratch_bytes(int m, int n, int k);
 // scratch: gemm_scratch_bytes(m, n, k) bytes, or nullptr (then no split: correct, slower)
+// bias (n floats) != nullptr: y = fl(O + b[j]) (+ relu): the encoder's linear layers
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
-                               int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream);
+                               int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
+                               const float *bias = nullptr, bool relu = false);
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
                            hipStream_t stream);
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
                          int64_t csh, int64_t csw, int m, int n, int k, hipStream_t stream);
+// batch of independent GEMMs (blockIdx.z), operand i at base + i * batch stride (attention heads)
+hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64_t a_bs, const float *B, int64_t bsh,
+                                 int64_t bsw, int64_t b_bs, float *C, int64_t csh, int64_t csw, int64_t c_bs, int m,
+                                 int n, int k, int batch, hipStream_t stream);
+// Encoder row ops (encoder_ops.hip): the reference's op_softmax (after op_multiply by `scale`) and
+// op_add + op_layernorm, one row per wave, sums in the reference's sequential order.
+hipError_t launch_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, hipStream_t stream);
+hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w,
+                                     hipStream_t stream);
+// The encoder counterpart (encoder.hip).
+struct Encoder;
+uint64_t encoder_weight_seed(uint64_t base, int block, int kind, int head);
+float encoder_init_bound(int n);
+hipError_t encoder_create(int d_model, int n_heads, int d_ff, int n_blocks, int max_seq, uint64_t seed, Encoder **out);
+hipError_t encoder_forward(Encoder *E, const float *X, float *Y, int seq, hipStream_t s);
+void encoder_destroy(Encoder *E);
 const char *gemm_config_name();
 // Quantization-error statistics on the device (error_stats.hip); scratch = error_stats_scratch_bytes().
 size_t error_stats_scratch_bytes();

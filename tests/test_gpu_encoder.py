@@ -1,0 +1,80 @@
+"""GPU parity of the encoder counterpart (BASELINE config 5) against the oracle.
+
+The encoder's quantized linears (Q/K/V, W_O, FFN with fused bias / relu), fp32 attention GEMMs,
+softmax and add + layernorm are each compared with the oracle restatement bit for bit, then the
+whole stack at the reference's own shape (transformer.cu:171-178), a small shape and config 5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from util import assert_bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, device):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+@pytest.mark.parametrize("rows,w", [(64, 7), (48, 64), (1024, 512), (5, 1000)])
+def test_softmax_rows_bit_exact(qg, oracle, device, rows, w):
+    S = oracle.uniform((rows, w), 3) * np.float32(8.0)
+    P = qg.softmax_rows(_dev(S, device), scale=0.125)
+    assert_bits_equal(P.cpu().numpy(), oracle.softmax_rows(S, 0.125), f"softmax {rows}x{w}")
+
+
+def test_softmax_in_place(qg, oracle, device):
+    S = oracle.uniform((256, 512), 4)
+    Sd = _dev(S, device)
+    qg.softmax_rows(Sd, scale=0.125, P=Sd)
+    assert_bits_equal(Sd.cpu().numpy(), oracle.softmax_rows(S, 0.125), "softmax in place")
+
+
+@pytest.mark.parametrize("rows,w", [(33, 8), (512, 1024), (7, 4096), (9, 100)])
+def test_add_layernorm_rows_bit_exact(qg, oracle, device, rows, w):
+    A, B = oracle.uniform((rows, w), 5), oracle.uniform((rows, w), 6)
+    Y = qg.add_layernorm_rows(_dev(A, device), _dev(B, device))
+    assert_bits_equal(Y.cpu().numpy(), oracle.add_layernorm_rows(A, B), f"add+layernorm {rows}x{w}")
+
+
+@pytest.mark.parametrize("M,N,K,bias,relu", [(100, 260, 300, True, True), (100, 260, 300, True, False),
+                                             (100, 260, 300, False, False), (512, 1024, 1024, True, True),
+                                             (512, 4096, 1024, True, False)])
+def test_linear_fused_bias_relu_bit_exact(qg, oracle, device, M, N, K, bias, relu):
+    X, W = oracle.inputs(M, N, K, 91)
+    b = oracle.uniform((N,), 92) if bias else None
+    pw = qg.pack_b(_dev(W, device))
+    Y = qg.linear(_dev(X, device), pw, bias=None if b is None else _dev(b, device), relu=relu)
+    assert_bits_equal(Y.cpu().numpy(), oracle.linear(X, W, b, relu), f"linear {M}x{N}x{K} b={bias} relu={relu}")
+
+
+@pytest.mark.parametrize("seq,d,H,dff,blocks", [
+    (6, 8, 4, 8, 2),          # the reference's own Encoder call (transformer.cu:171-178)
+    (32, 64, 4, 128, 2),
+    (100, 256, 8, 512, 3),    # ragged seq, odd block count
+])
+def test_encoder_forward_bit_exact(qg, oracle, device, seq, d, H, dff, blocks):
+    X = oracle.uniform((seq, d), 11)
+    enc = qg.Encoder(d, H, dff, blocks, max_seq=seq, seed=13)
+    try:
+        Y = enc.forward(_dev(X, device))
+        torch.cuda.synchronize()
+        want = oracle.encoder_forward(X, d, H, dff, blocks, 13)
+        assert_bits_equal(Y.cpu().numpy(), want, f"encoder seq={seq} d={d} H={H} dff={dff} blocks={blocks}")
+        Y2 = enc.forward(_dev(X, device))   # weights cached: a second call gives the same bits
+        assert_bits_equal(Y2.cpu().numpy(), want, "encoder second call")
+    finally:
+        enc.close()
+
+
+def test_encoder_config5_bit_exact(qg, oracle, device):
+    """BASELINE config 5: d_model 1024, seq 512 (16 heads, d_ff 4096, 2 blocks)."""
+    seq, d, H, dff, blocks = 512, 1024, 16, 4096, 2
+    X = oracle.uniform((seq, d), 17)
+    enc = qg.Encoder(d, H, dff, blocks, max_seq=seq, seed=19)
+    try:
+        Y = enc.forward(_dev(X, device)).cpu().numpy()
+    finally:
+        enc.close()
+    assert_bits_equal(Y, oracle.encoder_forward(X, d, H, dff, blocks, 19), "encoder config 5")

@@ -120,3 +120,75 @@ def test_generator_is_uniform(oracle):
     assert abs(float(u.mean())) < 0.01
     # 24 random bits: 2u-1 is exact, so every value is a multiple of 2^-23
     assert np.all(np.mod(u.astype(np.float64) * 2 ** 23, 1.0) == 0)
+
+
+# ---- encoder counterpart: the C restatement against literal per-element Python loops -----------
+
+def _literal_softmax_row(s, scale):
+    import math
+    f = np.float32
+    mx = f(f(s[0]) * f(scale))
+    for v in s[1:]:
+        x = f(f(v) * f(scale))
+        if x > mx:
+            mx = x
+    e = [f(math.exp(float(f(f(f(v) * f(scale)) - mx)))) for v in s]
+    tot = f(0.0)
+    for v in e:
+        tot = f(tot + v)
+    return np.array([f(v / tot) for v in e], np.float32)
+
+
+def _literal_add_layernorm_row(a, b):
+    f = np.float32
+    y = [f(f(x) + f(z)) for x, z in zip(a, b)]
+    mean = f(0.0)
+    for v in y:
+        mean = f(mean + v)
+    mean = f(mean / f(len(y)))
+    var = f(0.0)
+    for v in y:
+        d = f(v - mean)
+        var = f(var + f(d * d))
+    var = f(var / f(len(y)))
+    return np.array([f(f(v - mean) / var) for v in y], np.float32)
+
+
+def test_oracle_softmax_matches_literal(oracle):
+    S = oracle.uniform((5, 37), 21) * np.float32(6.0)
+    got = oracle.softmax_rows(S, 0.125)
+    for r in range(S.shape[0]):
+        assert np.array_equal(got[r].view(np.uint32), _literal_softmax_row(S[r], 0.125).view(np.uint32)), r
+
+
+def test_oracle_add_layernorm_matches_literal(oracle):
+    A, B = oracle.uniform((4, 50), 22), oracle.uniform((4, 50), 23)
+    got = oracle.add_layernorm_rows(A, B)
+    for r in range(A.shape[0]):
+        want = _literal_add_layernorm_row(A[r], B[r])
+        assert np.array_equal(got[r].view(np.uint32), want.view(np.uint32)), r
+
+
+def test_oracle_linear_is_quantized_mm_plus_bias_relu(oracle):
+    X, W = oracle.inputs(20, 30, 40, 24)
+    b = oracle.uniform((30,), 25)
+    O = oracle.quantized_mm(X, W)
+    y = (O + b).astype(np.float32)
+    assert np.array_equal(oracle.linear(X, W, b, False).view(np.uint32), y.view(np.uint32))
+    yr = np.where(y < 0, np.float32(0), y).astype(np.float32)
+    assert np.array_equal(oracle.linear(X, W, b, True).view(np.uint32), yr.view(np.uint32))
+
+
+def test_oracle_encoder_heads_concatenation_equals_per_head(oracle):
+    """Q/K/V for all heads from one quantized GEMM over [Wq^0 | ... | Wv^H-1] equal the per-head GEMMs
+    the reference runs (attention.cuh:54-56): the scales are per row of X and per column of W."""
+    d, H, seq = 16, 4, 6
+    dk = d // H
+    X = oracle.uniform((seq, d), 26)
+    bound = np.float32(1.0 / np.sqrt(np.float64(dk)))
+    heads = [oracle.uniform((d, dk), oracle.encoder_weight_seed(3, 0, 0, h), -bound, bound) for h in range(H)]
+    Wcat = np.concatenate(heads, axis=1)
+    full = oracle.quantized_mm(X, Wcat)
+    for h in range(H):
+        part = oracle.quantized_mm(X, heads[h])
+        assert np.array_equal(full[:, h * dk:(h + 1) * dk].view(np.uint32), part.view(np.uint32)), h
