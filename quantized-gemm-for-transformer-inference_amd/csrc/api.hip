@@ -69,19 +69,25 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Split-K scratch for qgemm_mm_packed (which has no workspace argument): grow-only, one per
 // (device, stream) -- the tickets and slabs are only safe to reuse in stream order.
+enum ScratchUse { kScratchSplitK = 0, kScratchErrorStats = 1 };  // never shared: split-K tickets must stay zero
 struct ScratchKey {
     int dev;
     hipStream_t stream;
-    bool operator<(const ScratchKey &o) const { return dev != o.dev ? dev < o.dev : stream < o.stream; }
+    int use;
+    bool operator<(const ScratchKey &o) const {
+        if (dev != o.dev) return dev < o.dev;
+        if (stream != o.stream) return stream < o.stream;
+        return use < o.use;
+    }
 };
 std::mutex g_scratch_mu;
 std::map<ScratchKey, CachedWs> g_scratch;
-hipError_t cached_scratch(size_t need, hipStream_t stream, void **out) {
+hipError_t cached_scratch(size_t need, hipStream_t stream, int use, void **out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    CachedWs &w = g_scratch[ScratchKey{dev, stream}];
+    CachedWs &w = g_scratch[ScratchKey{dev, stream, use}];
     if (w.bytes < need) {
         if (w.ptr) {
             if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
@@ -90,6 +96,7 @@ hipError_t cached_scratch(size_t need, hipStream_t stream, void **out) {
             w.bytes = 0;
         }
         if ((e = hipMalloc(&w.ptr, need)) != hipSuccess) return e;
+        if ((e = hipMemset(w.ptr, 0, need)) != hipSuccess) return e;  // split-K tickets start at zero
         w.bytes = need;
     }
     *out = w.ptr;
@@ -98,10 +105,10 @@ hipError_t cached_scratch(size_t need, hipStream_t stream, void **out) {
 
 hipError_t mm_packed_impl(const void *packed_a, const void *packed_b, float *C, int64_t c_stride_h,
                           int64_t c_stride_w, int m, int n, int k, float range, void *scratch, size_t scratch_bytes,
-                          hipStream_t stream) {
+                          hipStream_t stream, bool tickets_zeroed = false) {
     const float inv_r2 = 1.0f / (range * range);  // op_mm.cuh:99, one rounding per operation (host IEEE)
     return launch_gemm_dequant(packed_view(packed_a, m, k), packed_view(packed_b, n, k), C, c_stride_h, c_stride_w, m,
-                               n, inv_r2, scratch, scratch_bytes, stream);
+                               n, inv_r2, scratch, scratch_bytes, stream, nullptr, false, tickets_zeroed);
 }
 
 }  // namespace
@@ -145,10 +152,11 @@ int qgemm_mm_packed(const void *packed_a, const void *packed_b, float *C, int64_
     void *scratch = nullptr;
     const size_t sb = gemm_scratch_bytes(m, n, k);
     if (sb) {
-        hipError_t e = cached_scratch(sb, s, &scratch);
+        hipError_t e = cached_scratch(sb, s, kScratchSplitK, &scratch);
         if (e != hipSuccess) return err(e);
     }
-    return err(mm_packed_impl(packed_a, packed_b, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s));
+    return err(mm_packed_impl(packed_a, packed_b, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s,
+                              /*tickets_zeroed=*/true));
 }
 
 int qgemm_mm_packed_i32(const void *packed_a, const void *packed_b, int32_t *Acc, int m, int n, int k, void *stream) {
@@ -225,7 +233,7 @@ int qgemm_error_stats(const float *C, const float *O, int64_t count, int referen
     if (!C || !O || !stats || count < 1) return err(hipErrorInvalidValue);
     hipStream_t s = static_cast<hipStream_t>(stream);
     void *scratch = nullptr;
-    hipError_t e = cached_scratch(error_stats_scratch_bytes(), s, &scratch);
+    hipError_t e = cached_scratch(error_stats_scratch_bytes(), s, kScratchErrorStats, &scratch);
     if (e != hipSuccess) return err(e);
     return err(launch_error_stats(C, O, count, reference_order != 0, stats, scratch, s));
 }

@@ -88,7 +88,7 @@ hipError_t linear(Encoder &E, const float *x, int seq, int k, const void *wpacke
     if (e != hipSuccess) return e;
     const float inv_r2 = 1.0f / (127.0f * 127.0f);
     return launch_gemm_dequant(va, packed_view(wpacked, n, k), y, n, 1, seq, n, inv_r2, E.ws, E.scratch_bytes, s,
-                               bias, relu);
+                               bias, relu, /*tickets_zeroed=*/true);
 }
 
 }  // namespace
@@ -144,6 +144,7 @@ hipError_t encoder_create(int d_model, int n_heads, int d_ff, int n_blocks, int 
     E->scratch_bytes = (scratch + 255) & ~(size_t)255;
     E->ws_bytes = E->scratch_bytes + act;
     if ((e = alloc(reinterpret_cast<void **>(&E->ws), E->ws_bytes))) return fail(e);
+    if ((e = hipMemset(E->ws, 0, E->scratch_bytes))) return fail(e);  // split-K tickets start at zero
 
     // weights, drawn once with the reference's init bounds (attention.cuh:37-41, linear.cuh:34-39,
     // transformer.cu:53) and packed

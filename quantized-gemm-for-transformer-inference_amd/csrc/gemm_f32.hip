@@ -5,62 +5,95 @@
 // Bit-exact with the reference: every output is res = +0 then res = fmaf(a_k, b_k, res) for k
 // ascending (nvcc contracts :38), followed by the zero-padded products of the last 32-wide tile,
 // which only turn a -0 result into +0 (one fl(res + 0)).  Arbitrary strides (the Index() macro).
-// 64x64 tile per 256-thread block, 4x4 outputs per thread, k staged 16 at a time through LDS.
+// 128x128 or 64x64 tile per 256-thread block, k staged 16 at a time through LDS.
 #include "qgemm_internal.h"
 
 namespace qgemm {
 
 namespace {
 
-constexpr int TM = 64, TN = 64, TK = 16;
+constexpr int TK = 16;
 
+// Tile TM x TN per 256-thread block, (TM/16) x (TN/16) outputs per thread (rows ty*RM.., cols tx*RN..).
+// Operand tiles are staged through LDS as [k][row] / [k][col]; the global->LDS mapping follows the
+// operand's contiguous dimension, so row-major, transposed and head-sliced views all load coalesced.
+template <int TM, int TN>
 __global__ __launch_bounds__(256) void mm_f32_kernel(const float *__restrict__ A, int64_t ash, int64_t asw,
                                                      const float *__restrict__ B, int64_t bsh, int64_t bsw,
                                                      float *__restrict__ C, int64_t csh, int64_t csw, int m, int n,
                                                      int k, int64_t a_bs, int64_t b_bs, int64_t c_bs) {
+    constexpr int RM = TM / 16, RN = TN / 16;  // 16 x 16 threads
+    static_assert(RM >= 1 && RN >= 4 && RN % 4 == 0, "B fragment read as float4");
     // batch z (attention heads): operands offset by the batch strides
     A += blockIdx.z * a_bs;
     B += blockIdx.z * b_bs;
     C += blockIdx.z * c_bs;
-    __shared__ float As[TK][TM + 1];
-    __shared__ float Bs[TK][TN + 1];
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    __shared__ __attribute__((aligned(16))) float As[TK][TM + 4];
+    __shared__ __attribute__((aligned(16))) float Bs[TK][TN + 4];
+    const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
     const int64_t i0 = (int64_t)blockIdx.y * TM, j0 = (int64_t)blockIdx.x * TN;
-    float acc[4][4];
+    const bool a_kc = asw == 1;  // A's k is contiguous (row-major A)
+    const bool b_nc = bsw == 1;  // B's n is contiguous (row-major B); else k contiguous (B^T view)
+    float acc[RM][RN];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < RM; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = 0.0f;
-    for (int k0 = 0; k0 < k; k0 += TK) {
-        for (int e = threadIdx.x; e < TK * TM; e += 256) {
-            const int kk = e / TM, r = e % TM;  // A tile, stored [k][row]
+        for (int b = 0; b < RN; ++b) acc[a][b] = 0.0f;
+    constexpr int NA = TK * TM / 256, NB = TK * TN / 256;  // staged elements per thread
+    float ra[NA], rb[NB];
+    auto fetch = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int x = 0; x < NA; ++x) {
+            const int e = x * 256 + t;
+            const int kk = a_kc ? (e % TK) : (e / TM), r = a_kc ? (e / TK) : (e % TM);
             const int64_t gi = i0 + r, gk = k0 + kk;
-            As[kk][r] = (gi < m && gk < k) ? A[gi * ash + gk * asw] : 0.0f;
-            const int kb = e / TN, c = e % TN;  // B tile, stored [k][col]
-            const int64_t gj = j0 + c, gkb = k0 + kb;
-            Bs[kb][c] = (gj < n && gkb < k) ? B[gkb * bsh + gj * bsw] : 0.0f;
+            ra[x] = (gi < m && gk < k) ? A[gi * ash + gk * asw] : 0.0f;
         }
+#pragma unroll
+        for (int x = 0; x < NB; ++x) {
+            const int e = x * 256 + t;
+            const int kb = b_nc ? (e / TN) : (e % TK), c = b_nc ? (e % TN) : (e / TK);
+            const int64_t gj = j0 + c, gkb = k0 + kb;
+            rb[x] = (gj < n && gkb < k) ? B[gkb * bsh + gj * bsw] : 0.0f;
+        }
+    };
+    auto deposit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int x = 0; x < NA; ++x) {
+            const int e = x * 256 + t;
+            As[a_kc ? (e % TK) : (e / TM)][a_kc ? (e / TK) : (e % TM)] = ra[x];
+        }
+#pragma unroll
+        for (int x = 0; x < NB; ++x) {
+            const int e = x * 256 + t;
+            Bs[b_nc ? (e / TN) : (e % TK)][b_nc ? (e % TN) : (e / TK)] = rb[x];
+        }
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < k; k0 += TK) {
+        deposit();
         __syncthreads();
+        if (k0 + TK < k) fetch(k0 + TK);  // next tile's loads in flight during this tile's FMAs
         const int kmax = min(TK, k - k0);
         for (int kk = 0; kk < kmax; ++kk) {
-            float av[4], bv[4];
+            float av[RM], bv[RN];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) av[a] = As[kk][ty * 4 + a];
+            for (int a = 0; a < RM; ++a) av[a] = As[kk][ty * RM + a];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) bv[b] = Bs[kk][tx * 4 + b];
+            for (int b = 0; b < RN; b += 4) *reinterpret_cast<float4 *>(bv + b) = *reinterpret_cast<const float4 *>(&Bs[kk][tx * RN + b]);
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < RM; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) acc[a][b] = __fmaf_rn(av[a], bv[b], acc[a][b]);
+                for (int b = 0; b < RN; ++b) acc[a][b] = __fmaf_rn(av[a], bv[b], acc[a][b]);
         }
         __syncthreads();
     }
     const bool padded = (k % 32) != 0;  // reference: trailing fma(0, 0, res) products of the last tile
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < RM; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int64_t gi = i0 + ty * 4 + a, gj = j0 + tx * 4 + b;
+        for (int b = 0; b < RN; ++b) {
+            const int64_t gi = i0 + ty * RM + a, gj = j0 + tx * RN + b;
             if (gi < m && gj < n) C[gi * csh + gj * csw] = padded ? __fadd_rn(acc[a][b], 0.0f) : acc[a][b];
         }
 }
@@ -75,8 +108,18 @@ hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *
 hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64_t a_bs, const float *B, int64_t bsh,
                                  int64_t bsw, int64_t b_bs, float *C, int64_t csh, int64_t csw, int64_t c_bs, int m,
                                  int n, int k, int batch, hipStream_t stream) {
-    const dim3 grid((unsigned)((n + TN - 1) / TN), (unsigned)((m + TM - 1) / TM), (unsigned)batch);
-    mm_f32_kernel<<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs, c_bs);
+    // 128 x 128 tiles when they alone give >= 256 blocks, else 64 x 64 (k is never split: every
+    // output is one sequential fmaf chain; a 32 x 64 tile measured slower on the attention PV GEMM)
+    const int64_t big = (int64_t)((n + 127) / 128) * ((m + 127) / 128) * batch;
+    if (big >= 256) {
+        const dim3 grid((unsigned)((n + 127) / 128), (unsigned)((m + 127) / 128), (unsigned)batch);
+        mm_f32_kernel<128, 128><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs,
+                                                          c_bs);
+    } else {
+        const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((m + 63) / 64), (unsigned)batch);
+        mm_f32_kernel<64, 64><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs,
+                                                        c_bs);
+    }
     return hipGetLastError();
 }
 

@@ -68,19 +68,22 @@ static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
 
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw, int m,
                                int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
-                               const float *bias, bool relu) {
+                               const float *bias, bool relu, bool tickets_zeroed) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
-               inv_r2, 1, nullptr, nullptr, bias};
+               inv_r2, 1, nullptr, nullptr, bias, tickets_zeroed ? 1 : 0};
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
     const int splits = gemm_splits(m, n, (int)a.k_pad);
     if (splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
         p.splits = splits;
         p.tickets = static_cast<unsigned *>(scratch);
         p.slabs = reinterpret_cast<int32_t *>(static_cast<char *>(scratch) + ticket_bytes(tiles));
-        // the tickets are polled state: zeroed ahead of every launch (a memset node under capture)
-        hipError_t e = hipMemsetAsync(p.tickets, 0, ticket_bytes(tiles), stream);
-        if (e != hipSuccess) return e;
+        // the tickets are polled state: zeroed ahead of every launch (a memset node under capture) unless
+        // the scratch is library-owned, zeroed at allocation and re-zeroed by each launch's reducers
+        if (!tickets_zeroed) {
+            hipError_t e = hipMemsetAsync(p.tickets, 0, ticket_bytes(tiles), stream);
+            if (e != hipSuccess) return e;
+        }
     }
     const dim3 grid((unsigned)(tiles * p.splits));
     if (!bias) return launch_v3<kEpiNone>(p, grid, stream);
@@ -90,7 +93,7 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n, hipStream_t stream) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, Acc, n, 1, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
-               0.0f, 1, nullptr, nullptr, nullptr};
+               0.0f, 1, nullptr, nullptr, nullptr, 0};
     gemm_i8_v1<kStoreDirect, false><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
     return hipGetLastError();
 }

@@ -72,6 +72,7 @@ struct GemmArgs {
     int32_t *slabs;     // tiles x splits x (BM x BN) int32, MFMA-native order
     unsigned *tickets;  // tiles words, zeroed before every launch
     const float *bias;  // n floats, added after the dequantize (kEpi >= 1)
+    int reset_tickets;  // the reducer re-zeroes its ticket (scratch zeroed once at allocation)
 };
 
 // Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
@@ -406,6 +407,8 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, int8_t *lds, v
         if (t == (unsigned)(S - 1)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // every slice has arrived: nobody else touches this ticket in this launch
+            if (p.reset_tickets) __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();

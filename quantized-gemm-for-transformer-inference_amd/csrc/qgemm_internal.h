@@ -106,10 +106,12 @@ hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float l
 int gemm_splits(int m, int n, int k);
 size_t gemm_scratch_bytes(int m, int n, int k);
 // scratch: gemm_scratch_bytes(m, n, k) bytes, or nullptr (then no split: correct, slower)
-// bias (n floats) != nullptr: y = fl(O + b[j]) (+ relu): the encoder's linear layers
+// bias (n floats) != nullptr: y = fl(O + b[j]) (+ relu): the encoder's linear layers.
+// tickets_zeroed: the split-K scratch is library-owned, zeroed once at allocation; the launch's
+// reducers re-zero their tickets instead of a memset ahead of every launch.
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
                                int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
-                               const float *bias = nullptr, bool relu = false);
+                               const float *bias = nullptr, bool relu = false, bool tickets_zeroed = false);
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
                            hipStream_t stream);
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
