@@ -29,26 +29,49 @@ static bool shape_ok(const PackedView &a, const PackedView &b) {
     return a.k_pad == b.k_pad && a.rows_pad % BM == 0 && b.rows_pad % BN == 0 && a.k_pad % BK == 0;
 }
 
-// Slices per tile: enough blocks to cover the CUs (one 130-KiB-LDS block per CU), each slice at least
-// two k-steps, at most 8 slices.  Shapes with >= 160 tiles are not split.
-int gemm_splits(int m, int n, int k) {
-    if (m <= 0 || n <= 0 || k <= 0) return 1;
-    const int64_t tiles = (round_up(m, BM) / BM) * (round_up(n, BN) / BN);
+// Launch plan.  256 x 256 tiles (gemm_i8_v3) while they give >= 128 blocks; below that the 128 x 128
+// kernel (gemm_i8_t128, two blocks per CU).  Then split-K when the tiles alone leave CUs idle:
+// S = min(target blocks / tiles, k-steps / 2, 8) slices per tile (each slice >= 2 k-steps).
+struct GemmPlan {
+    int tile;       // 256 or 128
+    int tiles_m, tiles_n;
+    int splits;
+};
+
+static GemmPlan gemm_plan(int m, int n, int k) {
+    GemmPlan g{256, (int)(round_up(m, 256) / 256), (int)(round_up(n, 256) / 256), 1};
+    if (m <= 0 || n <= 0 || k <= 0) return g;
+    int target = 256, no_split = 160;
+    if ((int64_t)g.tiles_m * g.tiles_n < 128) {
+        g = GemmPlan{128, (int)(round_up(m, 128) / 128), (int)(round_up(n, 128) / 128), 1};
+        target = 512;
+        no_split = 320;
+    }
+    const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
     const int nk = (int)(round_up(k, BK) / BK);
-    if (tiles >= 160) return 1;
-    int s = (int)(256 / tiles);
-    s = s < nk / 2 ? s : nk / 2;
-    s = s < 8 ? s : 8;
-    return s > 1 ? s : 1;
+    if (tiles >= no_split) return g;
+    int sp = (int)(target / tiles);
+    sp = sp < nk / 2 ? sp : nk / 2;
+    sp = sp < 8 ? sp : 8;
+    g.splits = sp > 1 ? sp : 1;
+    return g;
 }
 
-static size_t ticket_bytes(int64_t tiles) { return (size_t)round_up(tiles * 4, 256); }
+int gemm_splits(int m, int n, int k) { return gemm_plan(m, n, k).splits; }
+
+// One fixed ticket region at the start of every split-K scratch (splits happen only below 320 tiles):
+// shapes that share a library-owned scratch then never write slabs over each other's tickets.
+constexpr size_t kTicketBytes = 4096;
+static size_t ticket_bytes(int64_t tiles) {
+    (void)tiles;
+    return kTicketBytes;
+}
 
 size_t gemm_scratch_bytes(int m, int n, int k) {
-    const int s = gemm_splits(m, n, k);
-    if (s <= 1) return 0;
-    const int64_t tiles = (round_up(m, BM) / BM) * (round_up(n, BN) / BN);
-    return ticket_bytes(tiles) + (size_t)tiles * s * kSlabInts * 4;
+    const GemmPlan g = gemm_plan(m, n, k);
+    if (g.splits <= 1) return 0;
+    const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
+    return ticket_bytes(tiles) + (size_t)tiles * g.splits * g.tile * g.tile * 4;
 }
 
 template <int kEpi>
@@ -66,16 +89,30 @@ static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     return e;
 }
 
+template <int kEpi>
+static hipError_t launch_t128(const GemmArgs &p, dim3 grid, hipStream_t stream) {
+    const GemmEvents ev = take_gemm_events();
+    if ((ev.start || ev.stop) && g_event_mode == 0) {
+        hipExtLaunchKernelGGL((gemm_i8_t128<kEpi>), grid, dim3(t128::kThreads), 0, stream, ev.start, ev.stop, 0, p);
+        return hipGetLastError();
+    }
+    if (ev.start) (void)hipEventRecord(ev.start, stream);
+    gemm_i8_t128<kEpi><<<grid, dim3(t128::kThreads), 0, stream>>>(p);
+    hipError_t e = hipGetLastError();
+    if (ev.stop) (void)hipEventRecord(ev.stop, stream);
+    return e;
+}
+
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw, int m,
                                int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
                                const float *bias, bool relu, bool tickets_zeroed) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
-    GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
+    const GemmPlan g = gemm_plan(m, n, (int)a.k_pad);
+    GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, g.tiles_m, g.tiles_n,
                inv_r2, 1, nullptr, nullptr, bias, tickets_zeroed ? 1 : 0};
-    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    const int splits = gemm_splits(m, n, (int)a.k_pad);
-    if (splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
-        p.splits = splits;
+    const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
+    if (g.splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
+        p.splits = g.splits;
         p.tickets = static_cast<unsigned *>(scratch);
         p.slabs = reinterpret_cast<int32_t *>(static_cast<char *>(scratch) + ticket_bytes(tiles));
         // the tickets are polled state: zeroed ahead of every launch (a memset node under capture) unless
@@ -86,6 +123,10 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
         }
     }
     const dim3 grid((unsigned)(tiles * p.splits));
+    if (g.tile == 128) {
+        if (!bias) return launch_t128<kEpiNone>(p, grid, stream);
+        return relu ? launch_t128<kEpiBiasRelu>(p, grid, stream) : launch_t128<kEpiBias>(p, grid, stream);
+    }
     if (!bias) return launch_v3<kEpiNone>(p, grid, stream);
     return relu ? launch_v3<kEpiBiasRelu>(p, grid, stream) : launch_v3<kEpiBias>(p, grid, stream);
 }

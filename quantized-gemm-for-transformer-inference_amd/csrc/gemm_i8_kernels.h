@@ -388,17 +388,19 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 // Correct for any placement of a tile's slices over XCDs/CUs.  The "last arriver" word goes through
 // the one LDS array (a second __shared__ object can de-pipeline the main loop).  Returns true in the
 // reducer, which then holds the complete sums in acc.
-__device__ __forceinline__ bool splitk_combine(const GemmArgs &p, int8_t *lds, v4i (&acc)[8][4], int tile, int slice,
-                                               int S, int wave, int lane, int tid) {
-    v4i *slabs = reinterpret_cast<v4i *>(p.slabs) + (int64_t)tile * S * (kSlabInts / 4);
-    v4i *mine = slabs + (int64_t)slice * (kSlabInts / 4) + wave * (32 * 64) + lane;
+// MI x NI accumulator tiles per wave, kWaves waves: a slab is kWaves*MI*NI*64 v4i (= the tile's int32s).
+template <int MI, int NI, int kWaves>
+__device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last, v4i (&acc)[MI][NI], int tile,
+                                               int slice, int S, int wave, int lane, int tid) {
+    constexpr int64_t kSlabV4 = (int64_t)kWaves * MI * NI * 64;
+    v4i *slabs = reinterpret_cast<v4i *>(p.slabs) + (int64_t)tile * S * kSlabV4;
+    v4i *mine = slabs + (int64_t)slice * kSlabV4 + wave * (MI * NI * 64) + lane;
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) mine[(mi * 4 + ni) * 64] = acc[mi][ni];
+        for (int ni = 0; ni < NI; ++ni) mine[(mi * NI + ni) * 64] = acc[mi][ni];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    unsigned *last = reinterpret_cast<unsigned *>(lds + kLdsBytes);
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -415,11 +417,11 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, int8_t *lds, v
     if (*last != (unsigned)(S - 1)) return false;
     for (int s = 0; s < S; ++s) {
         if (s == slice) continue;
-        const v4i *src = slabs + (int64_t)s * (kSlabInts / 4) + wave * (32 * 64) + lane;
+        const v4i *src = slabs + (int64_t)s * kSlabV4 + wave * (MI * NI * 64) + lane;
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) acc[mi][ni] += src[(mi * 4 + ni) * 64];
+            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += src[(mi * NI + ni) * 64];
     }
     return true;
 }
@@ -492,8 +494,159 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
         mfmas(a1, b1);
     }
 
-    if (S > 1 && !splitk_combine(p, lds, acc, tile, slice, S, wave, lane, tid)) return;
+    if (S > 1 &&
+        !splitk_combine<8, 4, 8>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice, S, wave, lane, tid))
+        return;
     epilogue16<kMode, kEpi>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// gemm_i8_t128: the 128 x 128 macro-tile for problems with few 256 x 256 tiles (the encoder's M = 512
+// linears, decode-sized M): 4 waves as 2 x 2, each 64 x 64 = 4 x 4 tiles of v_mfma_i32_16x16x64_i8,
+// the same staging (LDS-DMA, source-swizzled 128-B rows, 2-deep ring of 32-KiB stages), schedule and
+// split-K combine as gemm_i8_v3; the epilogue writes the whole 128 x 128 fp32 tile through the
+// 64-KiB ring at once.  Two blocks per CU.
+namespace t128 {
+constexpr int TB = 128;                       // macro-tile rows = cols
+constexpr int kThreads = 256;
+constexpr int kTileBytes = TB * BK;           // 16 KiB per operand per stage
+constexpr int kStageBytes = 2 * kTileBytes;
+constexpr int kLdsBytes = 2 * kStageBytes;    // 64 KiB
+}  // namespace t128
+
+template <int kEpi = kEpiNone>
+__global__ __launch_bounds__(t128::kThreads, 2) void gemm_i8_t128(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[t128::kLdsBytes + 2048];  // + Cx, Cw, bias (128 each) + flag
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int S = p.splits > 1 ? p.splits : 1;
+    const int wid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = wid / S, slice = wid - tile * S;
+    int tm, tn;
+    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
+    const int nk_all = (int)(p.k_pad / BK);
+    const int kt0 = slice * nk_all / S;
+    const int nk = (slice + 1) * nk_all / S - kt0;
+    // staging: wave w fills rows [32w, 32w+32) of both tiles, 8 rows (1 KiB) per LDS-DMA, chunk g of
+    // row r at slot g ^ ((r>>1)&7)
+    const int8_t *Ablk = p.A + (int64_t)tm * t128::TB * p.k_pad;
+    const int8_t *Bblk = p.B + (int64_t)tn * t128::TB * p.k_pad;
+    int64_t src_off[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = wave * 32 + i * 8 + (lane >> 3);
+        src_off[i] = (int64_t)row * p.k_pad + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+    }
+    auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
+        int8_t *la = lds + buf * t128::kStageBytes;
+        int8_t *lb = la + t128::kTileBytes;
+        const int8_t *ga = Ablk + (int64_t)kt * BK;
+        const int8_t *gb = Bblk + (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_global_load_lds((const void *)(ga + src_off[i]), (void *)(la + (wave * 32 + i * 8) * BK), 16,
+                                             0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(gb + src_off[i]), (void *)(lb + (wave * 32 + i * 8) * BK), 16,
+                                             0, 0);
+        }
+    };
+    const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
+    const int a_row0 = (wm * 64 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    int off[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+
+    v4i acc[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4i{};
+    auto read_frags = [&](v4i (&a)[4], v4i (&b)[4], int buf, int s) __attribute__((always_inline)) {
+        const int8_t *la = lds + buf * t128::kStageBytes;
+        const int8_t *lb = la + t128::kTileBytes;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[s]);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[s]);
+    };
+    auto mfmas = [&](const v4i (&a)[4], const v4i (&b)[4]) __attribute__((always_inline)) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    v4i a0[4], b0[4], a1[4], b1[4];
+    stage(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    read_frags(a0, b0, 0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) stage(kt0 + kt + 1, cur ^ 1);
+        read_frags(a1, b1, cur, 1);
+        mfmas(a0, b0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (more) read_frags(a0, b0, cur ^ 1, 0);
+        mfmas(a1, b1);
+    }
+
+    if (S > 1 &&
+        !splitk_combine<4, 4, 4>(p, reinterpret_cast<unsigned *>(lds + t128::kLdsBytes + 1536), acc, tile, slice, S, wave,
+                                 lane, tid))
+        return;
+
+    // epilogue: the whole fp32 tile through LDS, then 512-B row stores
+    const int gi0 = tm * t128::TB, gj0 = tn * t128::TB;
+    float *sCx = reinterpret_cast<float *>(lds + t128::kLdsBytes);
+    float *sCw = sCx + t128::TB;
+    float *sB = sCw + t128::TB;
+    __syncthreads();  // every wave is done with the staging ring
+    if (tid < t128::TB) sCx[tid] = p.Cx[gi0 + tid];
+    else sCw[tid - t128::TB] = p.Cw[gj0 + tid - t128::TB];
+    if constexpr (kEpi >= kEpiBias)
+        if (tid < t128::TB) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
+    __syncthreads();
+    float *T = reinterpret_cast<float *>(lds);  // [128][128] fp32 = the 64-KiB ring
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int jl = wn * 64 + ni * 16 + lrow;
+        const float cw = sCw[jl];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int il = wm * 64 + mi * 16 + 4 * kq + r;
+                T[il * t128::TB + jl] = epi_extra<kEpi>(dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2), sB,
+                                                  jl);
+            }
+    }
+    __syncthreads();
+    float *C = static_cast<float *>(p.C);
+    const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
+                      gj0 + t128::TB <= p.n;
+    const int c4 = (tid & 31) * 4;
+#pragma unroll 4
+    for (int rr = tid >> 5; rr < t128::TB; rr += t128::kThreads / 32) {
+        const int i = gi0 + rr;
+        if (i >= p.m) break;
+        const float4 v = *reinterpret_cast<const float4 *>(T + rr * t128::TB + c4);
+        const int j = gj0 + c4;
+        if (full) {
+            *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = v;
+        } else {
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+        }
+    }
 }
 
 

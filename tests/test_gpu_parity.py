@@ -100,6 +100,21 @@ def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
     assert_bits_equal(_run_full(qg, X, W, device), want, f"{M}x{N}x{K} op_quantized_mm")
 
 
+def test_split_k_shapes_share_library_scratch(qg, oracle, device):
+    """Different split-K plans one after another on the same stream share qgemm_mm_packed's scratch
+    (tickets zeroed once, re-zeroed by each launch's reducers): every call stays bit-exact."""
+    shapes = [(512, 3072, 1024), (512, 1024, 4096), (256, 256, 2048), (512, 3072, 1024), (512, 1024, 4096)]
+    cache = {}
+    for i, (M, N, K) in enumerate(shapes):
+        if (M, N, K) not in cache:
+            X, W = oracle.inputs(M, N, K, 101 + len(cache))
+            cache[(M, N, K)] = (X, W, oracle.quantized_mm(X, W))
+        X, W, want = cache[(M, N, K)]
+        O = qg.mm_packed(qg.pack_a(_dev(X, device)), qg.pack_b(_dev(W, device)))
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"call {i}: {M}x{N}x{K}")
+
+
 def test_device_generator_matches_oracle(qg, oracle, device):
     t = torch.empty(1 << 20, device=device)
     qg.fill_uniform(t, seed=9)
