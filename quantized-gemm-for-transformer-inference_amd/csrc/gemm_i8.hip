@@ -31,7 +31,9 @@ static bool shape_ok(const PackedView &a, const PackedView &b) {
 
 // Launch plan.  256 x 256 tiles (gemm_i8_v3) while they give >= 128 blocks; below that the 128 x 128
 // kernel (gemm_i8_t128, two blocks per CU).  Then split-K when the tiles alone leave CUs idle:
-// S = min(target blocks / tiles, k-steps / 2, 8) slices per tile (each slice >= 2 k-steps).
+// S = min(256 / tiles, k-steps / 8, 8) slices per tile -- every slice keeps >= 8 k-steps (K >= 1024),
+// since the slab round trip costs ~3-5 us (scripts/split_probe.py: at M = 512, K = 1024 every split
+// was slower; K = 4096 split 4 was fastest; 2048^3 on 128-tiles unsplit beat split 2).
 struct GemmPlan {
     int tile;       // 256 or 128
     int tiles_m, tiles_n;
@@ -41,17 +43,17 @@ struct GemmPlan {
 static GemmPlan gemm_plan(int m, int n, int k) {
     GemmPlan g{256, (int)(round_up(m, 256) / 256), (int)(round_up(n, 256) / 256), 1};
     if (m <= 0 || n <= 0 || k <= 0) return g;
-    int target = 256, no_split = 160;
+    const int target = 256;
+    int no_split = 160;
     if ((int64_t)g.tiles_m * g.tiles_n < 128) {
         g = GemmPlan{128, (int)(round_up(m, 128) / 128), (int)(round_up(n, 128) / 128), 1};
-        target = 512;
-        no_split = 320;
+        no_split = 256;
     }
     const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
     const int nk = (int)(round_up(k, BK) / BK);
     if (tiles >= no_split) return g;
     int sp = (int)(target / tiles);
-    sp = sp < nk / 2 ? sp : nk / 2;
+    sp = sp < nk / 8 ? sp : nk / 8;
     sp = sp < 8 ? sp : 8;
     g.splits = sp > 1 ? sp : 1;
     return g;

@@ -389,39 +389,45 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 // the one LDS array (a second __shared__ object can de-pipeline the main loop).  Returns true in the
 // reducer, which then holds the complete sums in acc.
 // MI x NI accumulator tiles per wave, kWaves waves: a slab is kWaves*MI*NI*64 v4i (= the tile's int32s).
+// Publish form (cdna_hip_programming.md s5 'In-launch split-K reduction', the write-through variant):
+// slab stores are sc1 (write-through), drained by every wave before the block barrier, then lane 0
+// draws the ticket with a relaxed agent-scope add -- no release fence (a buffer_wbl2 would also write
+// back every dirty line of the XCD's L2, including other blocks' output tiles); the reducer reads
+// the other slabs with sc1 loads (every load of them), so no acquire either.
 template <int MI, int NI, int kWaves>
 __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last, v4i (&acc)[MI][NI], int tile,
                                                int slice, int S, int wave, int lane, int tid) {
-    constexpr int64_t kSlabV4 = (int64_t)kWaves * MI * NI * 64;
-    v4i *slabs = reinterpret_cast<v4i *>(p.slabs) + (int64_t)tile * S * kSlabV4;
-    v4i *mine = slabs + (int64_t)slice * kSlabV4 + wave * (MI * NI * 64) + lane;
+    constexpr int kSlabBytes = kWaves * MI * NI * 64 * 16;
+    // one descriptor over this tile's S slabs (wave-uniform base)
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char *>(p.slabs) + (int64_t)tile * S * kSlabBytes, 0, S * kSlabBytes, 0x00020000);
+    const int lane_off = (wave * (MI * NI * 64) + lane) * 16;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) mine[(mi * NI + ni) * 64] = acc[mi][ni];
+        for (int ni = 0; ni < NI; ++ni)
+            __builtin_amdgcn_raw_buffer_store_b128(acc[mi][ni], rsrc, slice * kSlabBytes + lane_off + (mi * NI + ni) * 1024,
+                                                   0, 16 /* sc1 */);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned t = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last = t;
-        if (t == (unsigned)(S - 1)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // every slice has arrived: nobody else touches this ticket in this launch
-            if (p.reset_tickets) __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        // every slice has arrived: nobody else touches this ticket in this launch
+        if (t == (unsigned)(S - 1) && p.reset_tickets)
+            __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (*last != (unsigned)(S - 1)) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: loads stay below
     for (int s = 0; s < S; ++s) {
         if (s == slice) continue;
-        const v4i *src = slabs + (int64_t)s * kSlabV4 + wave * (MI * NI * 64) + lane;
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += src[(mi * NI + ni) * 64];
+            for (int ni = 0; ni < NI; ++ni)
+                acc[mi][ni] += __builtin_amdgcn_raw_buffer_load_b128(rsrc, s * kSlabBytes + lane_off + (mi * NI + ni) * 1024,
+                                                                     0, 16 /* sc1 */);
     }
     return true;
 }
