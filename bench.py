@@ -41,6 +41,9 @@ CONFIGS = {
     "c3_up": (2048, 16384, 4096, "FFN up 2048x4096->16384 (BASELINE configs[2])"),
     "c3_down": (2048, 4096, 16384, "FFN down 2048x16384->4096 (BASELINE configs[2])"),
     "c4_shard": (8192, 4096, 4096, "M=65536 K=N=4096 / 8 GPUs, one 8192-row shard (BASELINE configs[3])"),
+    # encoder forward: (seq, d_model, n_heads, d_ff, n_blocks)
+    "c5_encoder": (512, 1024, 16, 4096, 2, "encoder forward d_model=1024 seq=512 (BASELINE configs[4]), 16 heads, "
+                   "d_ff 4096, 2 blocks; quantized Q/K/V, W_O, FFN linears"),
 }
 
 
@@ -162,6 +165,8 @@ def main():
 
     qg = load_pkg()
     L = qg.load()
+    if args.config == "c5_encoder":
+        return bench_encoder(args, qg, L, dev, world, rank, distributed)
     M, N, K, desc = CONFIGS[args.config]
 
     # inputs resident in HBM before timing; X differs per rank (its M-shard), W is replicated
@@ -281,6 +286,97 @@ def main():
         result["cpu_baseline"] = cpu_baseline(M, N, K, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def bench_encoder(args, qg, L, dev, world, rank, distributed):
+    """BASELINE config 5: the encoder counterpart's forward (seeded weights packed once, the
+    activations' quantize inside every forward); one forward per step, each rank its own sequence."""
+    import torch
+    import torch.distributed as dist
+    seq, d, H, dff, blocks, desc = CONFIGS["c5_encoder"]
+    enc = qg.Encoder(d, H, dff, blocks, max_seq=seq, seed=1000)
+    X = qg.fill_uniform(torch.empty((seq, d), device=dev), seed=2 * (1000 + rank))
+    Y = torch.empty_like(X)
+    hip = HipEvents(2 * args.steps)
+    L.qgemm_set_event_mode(0)
+    every = max(1, args.gemm_timing_every)
+    timed = [i for i in range(args.steps) if i % every == 0]
+    for _ in range(args.warmup):
+        enc.forward(X, Y)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if i % every == 0:  # times the forward's first GEMM: the fused Q/K/V projection
+            L.qgemm_set_gemm_events(hip.ev[2 * i], hip.ev[2 * i + 1])
+        enc.forward(X, Y)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gemm_ms = sum(hip.elapsed_ms(hip.ev[2 * i], hip.ev[2 * i + 1]) for i in timed) / len(timed)
+    hip.destroy()
+    if distributed:
+        t = torch.tensor([elapsed, gemm_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gemm_ms = float(t[0]), float(t[1])
+    qkv_ops = 2.0 * seq * 3 * d * d
+    lin_ops = blocks * 2.0 * seq * (3 * d * d + d * d + 2 * d * dff)
+    attn_flops = blocks * 2.0 * 2 * H * seq * seq * (d // H)
+    achieved = qkv_ops / (gemm_ms * 1e-3) / 1e12
+    result = {
+        "metric": "encoder forwards/s (BASELINE configs[4])",
+        "value": round(world * args.steps / elapsed, 2),
+        "unit": "forwards/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic U(-1,1) fp32 input, seeded weights (qgemm_fill_uniform streams)",
+        "config": {"workload": desc, "seq": seq, "d_model": d, "n_heads": H, "d_ff": dff, "n_blocks": blocks,
+                   "parallelism": f"independent sequences x{world}"},
+        "tokens_per_s": round(world * args.steps * seq / elapsed, 1),
+        "int8_tops_linears": round(lin_ops * args.steps / elapsed / 1e12, 2),
+        "fp32_tflops_attention": round(attn_flops * args.steps / elapsed / 1e12, 2),
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": round(PEAK_INT8_TOPS, 1),
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_INT8_TOPS, 4),
+            "traffic": None,
+            "kernel": "gemm_i8_t128 (fused Q/K/V projection, 512 x 3072 x 1024)",
+            "timing": f"hipExtLaunchKernel start/stop events on {len(timed)} of the {args.steps} timed forwards",
+        },
+        "library": qg.version(),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        O.build()
+        Xh = O.uniform((seq, d), 2 * 1000)
+        O.encoder_forward(Xh, d, H, dff, 1, 1000)  # warm
+        reps, tc = 0, 0.0
+        while tc < args.cpu_seconds and reps < 100:
+            c0 = time.perf_counter()
+            O.encoder_forward(Xh, d, H, dff, blocks, 1000)
+            tc += time.perf_counter() - c0
+            reps += 1
+        result["cpu_baseline"] = {
+            "value": reps / tc, "unit": "forwards/s",
+            "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), "kind": "port",
+            "sample": f"oracle/ C restatement of the encoder (transformer.cu:14-77 with quantized linears), "
+                      f"full config-5 forward x{reps} = {tc:.1f} s",
+        }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    enc.close()
     if distributed:
         dist.destroy_process_group()
 
