@@ -81,7 +81,7 @@ def test_invalid_pack_and_workspace_calls(qg):
 
 
 def test_harness_binaries_built(qg):
-    for exe in ("test_quantize", "timing_quantize"):
+    for exe in ("test_quantize", "timing_quantize", "transformer"):
         p = os.path.join(qg.PKG_DIR, "build", exe)
         assert os.access(p, os.X_OK), p
 

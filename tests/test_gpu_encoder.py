@@ -78,3 +78,22 @@ def test_encoder_config5_bit_exact(qg, oracle, device):
     finally:
         enc.close()
     assert_bits_equal(Y, oracle.encoder_forward(X, d, H, dff, blocks, 19), "encoder config 5")
+
+
+def test_transformer_harness_matches_oracle(qg, oracle):
+    """build/transformer (the reference main's Encoder call, transformer.cu:170-178) prints the same
+    output as the oracle on its input (first op_uniform_init draw) and weight seed."""
+    import os
+    import subprocess
+    exe = os.path.join(qg.PKG_DIR, "build", "transformer")
+    out = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=120).stdout
+    lines = [ln.strip() for ln in out.splitlines()]
+    seed = int(next(ln for ln in lines if ln.startswith("weight seed:")).split()[-1])
+    o = lines.index("output:")
+    got = [ln.split() for ln in lines[o + 1:o + 7]]
+    X = oracle.uniform((6, 8), 0)  # randgen_seed 0, first draw (op_mm_quantize.cuh op_uniform_init)
+    x = lines.index("X:")
+    assert [ln.split() for ln in lines[x + 1:x + 7]] == [[f"{v:.6f}" for v in row] for row in X]
+    want = oracle.encoder_forward(X, 8, 4, 8, 2, seed)
+    assert got == [[f"{v:.6f}" for v in row] for row in want]
+    assert "All tests completed successfully!" in lines
