@@ -114,6 +114,19 @@ QGEMM_API int qgemm_encoder_create(int d_model, int n_heads, int d_ff, int n_blo
 QGEMM_API int qgemm_encoder_forward(void *encoder, const float *X, float *Y, int seq, void *stream);
 QGEMM_API int qgemm_encoder_destroy(void *encoder);
 
+/* ---- LLM.int8() outlier decomposition ------------------------------------------
+ * Feature columns k of A (= rows of B) holding an element with NOT(|x| <= threshold) (the reference's
+ * AbsCompareLTEConstFunc, op_elemwise.cuh:293-306; NaN counts as an outlier) are multiplied in fp32,
+ * the rest by the int8 chain, so outliers no longer set the absmax scales:
+ *   C = fl( op_quantized_mm(A', B') + fmaf-chain over the outlier columns in ascending k )
+ * with A' / B' = A / B with those columns / rows zeroed (no outlier column: the plain op_mm_quantize).
+ * A: m x k, B: k x n, C: m x n, row-major contiguous, device pointers.  threshold: 6.0 in LLM.int8(). */
+QGEMM_API size_t qgemm_mm_outlier_workspace_size(int m, int n, int k);
+QGEMM_API int qgemm_mm_outlier(const float *A, const float *B, float *C, int m, int n, int k, float threshold,
+                     void *workspace, size_t ws_bytes, void *stream);
+/* number of outlier columns found by the last qgemm_mm_outlier on this workspace (synchronizes) */
+QGEMM_API int qgemm_outlier_count(int k, const void *workspace, int *count);
+
 /* The reference's quantization-error metric on the device: E = fl(C - O) per
  * element (op_subtract, op_elemwise.cuh:531-542), C = the unquantized product, O = the quantized one;
  * count elements, contiguous.  stats = DEVICE array of 5 doubles:

@@ -72,6 +72,8 @@ def lib():
             L.oracle_encoder_weight_seed.restype = _c_u64
             L.oracle_encoder_weight_seed.argtypes = [_c_u64, _c_int, _c_int, _c_int]
             L.oracle_encoder_forward.argtypes = [_f32p, _f32p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_u64]
+            L.oracle_mm_outlier.restype = _c_int
+            L.oracle_mm_outlier.argtypes = [_f32p, _f32p, _f32p, _c_int, _c_int, _c_int, _c_f]
             _lib = L
     return _lib
 
@@ -233,3 +235,13 @@ def encoder_forward(X, d_model: int, n_heads: int, d_ff: int, n_blocks: int, see
     Y = np.empty_like(X)
     lib().oracle_encoder_forward(X, Y, seq, d_model, n_heads, d_ff, n_blocks, seed)
     return Y
+
+
+def mm_outlier(X, W, threshold: float = 6.0):
+    """LLM.int8() decomposition: returns (O, number of outlier columns)."""
+    X, W = _c(X, np.float32), _c(W, np.float32)
+    M, K = X.shape
+    N = W.shape[1]
+    O = np.empty((M, N), np.float32)
+    cnt = lib().oracle_mm_outlier(X, W, O, M, N, K, float(threshold))
+    return O, int(cnt)

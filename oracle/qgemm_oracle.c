@@ -484,3 +484,45 @@ void oracle_encoder_forward(const float *X, float *Y, int seq, int d, int H, int
     free(one);
     free(b);
 }
+
+/* =================================================================================
+ * LLM.int8() outlier decomposition (the reference's unused hooks
+ * AbsCompareLTEConstFunc op_elemwise.cuh:293-306 and op_outlier_extractor :698-708).
+ * Column k of X is an outlier column when some X[i,k] is not in [-t, t] (NaN included);
+ * O = fl(quantized_mm(X', W') + fmaf chain over the outlier columns in ascending k), X'/W' with
+ * those columns/rows zeroed.  Returns the number of outlier columns.
+ * ================================================================================= */
+int oracle_mm_outlier(const float *X, const float *W, float *O, int M, int N, int K, float t)
+{
+    unsigned char *flag = (unsigned char *)calloc((size_t)K, 1);
+    for (int i = 0; i < M; ++i)
+        for (int k = 0; k < K; ++k) {
+            float a = X[(int64_t)i * K + k];
+            int inside = ((a >= 0) & (a <= t)) | ((a <= 0) & (-a <= t));
+            if (!inside) flag[k] = 1;
+        }
+    int *idx = (int *)malloc(sizeof(int) * (size_t)K);
+    int cnt = 0;
+    for (int k = 0; k < K; ++k)
+        if (flag[k]) idx[cnt++] = k;
+    float *Xm = (float *)malloc(sizeof(float) * (size_t)M * K);
+    float *Wm = (float *)malloc(sizeof(float) * (size_t)K * N);
+    for (int64_t e = 0; e < (int64_t)M * K; ++e) Xm[e] = flag[e % K] ? 0.0f : X[e];
+    for (int64_t e = 0; e < (int64_t)K * N; ++e) Wm[e] = flag[e / N] ? 0.0f : W[e];
+    oracle_quantized_mm(Xm, Wm, O, M, N, K, 127.0f);
+    if (cnt) {
+#pragma omp parallel for schedule(static)
+        for (int i = 0; i < M; ++i)
+            for (int j = 0; j < N; ++j) {
+                float acc = 0.0f;
+                for (int q = 0; q < cnt; ++q)
+                    acc = fmaf(X[(int64_t)i * K + idx[q]], W[(int64_t)idx[q] * N + j], acc);
+                O[(int64_t)i * N + j] = O[(int64_t)i * N + j] + acc;
+            }
+    }
+    free(flag);
+    free(idx);
+    free(Xm);
+    free(Wm);
+    return cnt;
+}

@@ -54,6 +54,9 @@ EXPORTED_SYMBOLS = (
     "qgemm_encoder_create",
     "qgemm_encoder_forward",
     "qgemm_encoder_destroy",
+    "qgemm_mm_outlier_workspace_size",
+    "qgemm_mm_outlier",
+    "qgemm_outlier_count",
     "qgemm_set_gemm_events",
     "qgemm_set_event_mode",
     "qgemm_fill_uniform",
@@ -128,6 +131,12 @@ def load() -> ctypes.CDLL:
         L.qgemm_encoder_forward.restype = i32
         L.qgemm_encoder_destroy.argtypes = [vp]
         L.qgemm_encoder_destroy.restype = i32
+        L.qgemm_mm_outlier_workspace_size.argtypes = [i32, i32, i32]
+        L.qgemm_mm_outlier_workspace_size.restype = sz
+        L.qgemm_mm_outlier.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, sz, vp]
+        L.qgemm_mm_outlier.restype = i32
+        L.qgemm_outlier_count.argtypes = [i32, vp, ctypes.POINTER(i32)]
+        L.qgemm_outlier_count.restype = i32
         L.qgemm_fill_uniform.argtypes = [vp, i64, ctypes.c_uint64, f32, f32, vp]
         L.qgemm_fill_uniform.restype = i32
         L.qgemm_set_gemm_events.argtypes = [vp, vp]
@@ -347,6 +356,28 @@ def add_layernorm_rows(A, B, Y=None):
                                                                       A.numel() // A.shape[-1], A.shape[-1],
                                                                       _stream(A.device)))
     return Y
+
+
+def mm_outlier(A, B, threshold: float = 6.0, C=None):
+    """LLM.int8() decomposition: outlier feature columns in fp32, the rest int8.
+    Returns (C, number of outlier columns)."""
+    import torch
+    _require_device_f32(A, "A")
+    _require_device_f32(B, "B")
+    assert A.is_contiguous() and B.is_contiguous()
+    M, K = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == K
+    if C is None:
+        C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    L = load()
+    ws = torch.empty(L.qgemm_mm_outlier_workspace_size(M, N, K), dtype=torch.uint8, device=A.device)
+    _check("qgemm_mm_outlier", L.qgemm_mm_outlier(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, float(threshold),
+                                                  ws.data_ptr(), ws.numel(), _stream(A.device)))
+    cnt = ctypes.c_int()
+    torch.cuda.current_stream(A.device).synchronize()
+    _check("qgemm_outlier_count", L.qgemm_outlier_count(K, ws.data_ptr(), ctypes.byref(cnt)))
+    return C, cnt.value
 
 
 ENCODER_WEIGHT_KINDS = ("Wq", "Wk", "Wv", "Wo", "W1", "b1", "W2", "b2")

@@ -289,6 +289,35 @@ int qgemm_encoder_destroy(void *encoder) {
     return 0;
 }
 
+size_t qgemm_mm_outlier_workspace_size(int m, int n, int k) {
+    if (!dims_ok(m, n, k)) return 0;
+    return align256(outlier_scratch_bytes(m, n, k)) + op_mm_quantize_workspace_size(m, n, k);
+}
+
+int qgemm_mm_outlier(const float *A, const float *B, float *C, int m, int n, int k, float threshold, void *workspace,
+                     size_t ws_bytes, void *stream) {
+    if (!A || !B || !C || !dims_ok(m, n, k) || !(threshold >= 0.0f)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    const size_t need = qgemm_mm_outlier_workspace_size(m, n, k);
+    if (!workspace || ws_bytes < need) return err(hipErrorInvalidValue);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    char *scratch = static_cast<char *>(workspace);
+    char *ws2 = scratch + align256(outlier_scratch_bytes(m, n, k));
+    float *Xm = nullptr, *Wm = nullptr;
+    hipError_t e = outlier_prepare(A, k, B, n, m, n, k, threshold, scratch, &Xm, &Wm, s);
+    if (e != hipSuccess) return err(e);
+    // the int8 part on the outlier-free operands (their scales no longer see the outliers)
+    const int rc = op_mm_quantize_ws(Xm, k, 1, Wm, n, 1, C, n, 1, m, n, k, kDefaultRange, ws2,
+                                     op_mm_quantize_workspace_size(m, n, k), stream);
+    if (rc) return rc;
+    return err(outlier_finish(A, k, B, n, m, n, k, scratch, C, n, s));
+}
+
+int qgemm_outlier_count(int k, const void *workspace, int *count) {
+    if (!workspace || !count || k < 1) return err(hipErrorInvalidValue);
+    return outlier_count_slot(k, workspace, count);
+}
+
 int qgemm_set_gemm_events(void *start_event, void *stop_event) {
     set_gemm_events(static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event));
     return 0;

@@ -125,6 +125,13 @@ hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64
 hipError_t launch_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, hipStream_t stream);
 hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w,
                                      hipStream_t stream);
+// LLM.int8() outlier decomposition (outlier.hip).
+size_t outlier_scratch_bytes(int m, int n, int k);
+hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, float t,
+                           void *scratch, float **Xm, float **Wm, hipStream_t s);
+hipError_t outlier_finish(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, void *scratch,
+                          float *O, int64_t osh, hipStream_t s);
+int outlier_count_slot(int k, const void *scratch, int *count_host);
 // The encoder counterpart (encoder.hip).
 struct Encoder;
 uint64_t encoder_weight_seed(uint64_t base, int block, int kind, int head);
