@@ -5,19 +5,19 @@
 // Bit-exact with the reference: every output is res = +0 then res = fmaf(a_k, b_k, res) for k
 // ascending (nvcc contracts :38), followed by the zero-padded products of the last 32-wide tile,
 // which only turn a -0 result into +0 (one fl(res + 0)).  Arbitrary strides (the Index() macro).
-// 128x128 or 64x64 tile per 256-thread block, k staged 16 at a time through LDS.
+// 128x128 or 64x64 tile per 256-thread block, k staged 16 or 64 at a time through LDS (64: a whole
+// tile's loads in flight per round trip -- the attention PV GEMM is latency-bound at 128 blocks).
 #include "qgemm_internal.h"
 
 namespace qgemm {
 
 namespace {
 
-constexpr int TK = 16;
 
 // Tile TM x TN per 256-thread block, (TM/16) x (TN/16) outputs per thread (rows ty*RM.., cols tx*RN..).
 // Operand tiles are staged through LDS as [k][row] / [k][col]; the global->LDS mapping follows the
 // operand's contiguous dimension, so row-major, transposed and head-sliced views all load coalesced.
-template <int TM, int TN>
+template <int TM, int TN, int TK>
 __global__ __launch_bounds__(256) void mm_f32_kernel(const float *__restrict__ A, int64_t ash, int64_t asw,
                                                      const float *__restrict__ B, int64_t bsh, int64_t bsw,
                                                      float *__restrict__ C, int64_t csh, int64_t csw, int m, int n,
@@ -108,17 +108,22 @@ hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *
 hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64_t a_bs, const float *B, int64_t bsh,
                                  int64_t bsw, int64_t b_bs, float *C, int64_t csh, int64_t csw, int64_t c_bs, int m,
                                  int n, int k, int batch, hipStream_t stream) {
-    // 128 x 128 tiles when they alone give >= 256 blocks, else 64 x 64 (k is never split: every
-    // output is one sequential fmaf chain; a 32 x 64 tile measured slower on the attention PV GEMM)
+    // 128 x 128 tiles only for >= 1024 such blocks, else 64 x 64 (more waves per SIMD to hide the load
+    // latency: attention QK^T 29 -> 19 us); k is never split: every output is one sequential fmaf
+    // chain (a 32 x 64 tile measured slower on the attention PV GEMM)
     const int64_t big = (int64_t)((n + 127) / 128) * ((m + 127) / 128) * batch;
-    if (big >= 256) {
+    if (big >= 1024) {
         const dim3 grid((unsigned)((n + 127) / 128), (unsigned)((m + 127) / 128), (unsigned)batch);
-        mm_f32_kernel<128, 128><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs,
+        mm_f32_kernel<128, 128, 16><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs,
                                                           c_bs);
     } else {
         const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((m + 63) / 64), (unsigned)batch);
-        mm_f32_kernel<64, 64><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs, b_bs,
-                                                        c_bs);
+        if (k >= 256)  // long chains: a whole 64-deep k tile per load round trip (attention PV)
+            mm_f32_kernel<64, 64, 64><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs,
+                                                                b_bs, c_bs);
+        else           // short k (attention QK^T, k = d_k): 16-deep tiles, next one prefetched
+            mm_f32_kernel<64, 64, 16><<<grid, 256, 0, stream>>>(A, ash, asw, B, bsh, bsw, C, csh, csw, m, n, k, a_bs,
+                                                                b_bs, c_bs);
     }
     return hipGetLastError();
 }
