@@ -127,6 +127,76 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     if (lane == 0) scale[row] = cx;
 }
 
+// pack_rows, long rows (4096 < len <= 16384): ONE 256-thread block per row, up to 16 float4 per
+// thread in registers (4-KiB coalesced loads per block instruction), block-wide absmax (shuffle + LDS),
+// quantized from the registers -- one HBM read of the row.  `red` holds >= 5 floats of LDS.
+constexpr int kLongRowMax = 16384;
+__device__ __forceinline__ void pack_row_block_body(int64_t row, const float *__restrict__ src, int64_t sh, int rows,
+                                                    int len, float range, float *__restrict__ scale,
+                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
+                                                    float *red) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (row >= rows_pad) return;
+    uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+    const int64_t nq = k_pad >> 2;
+    if (row >= rows) {  // padding row
+        for (int64_t c = t; c < nq; c += 256) qrow[c] = 0u;
+        if (t == 0) scale[row] = 0.0f;
+        return;
+    }
+    const float *srow = src + row * sh;
+    const float4 *s4 = reinterpret_cast<const float4 *>(srow);
+    const int nfull = len >> 2;
+    float4 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int c = t + 256 * j;
+        v[j] = (c < nfull) ? s4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float p = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int c = t + 256 * j;
+        if (c < nfull) {
+            p = (c == 0) ? p : cand_max(p, v[j].x);  // element 0 is the seed
+            p = cand_max(p, v[j].y);
+            p = cand_max(p, v[j].z);
+            p = cand_max(p, v[j].w);
+        }
+    }
+    const int tail0 = nfull << 2;
+    if (tail0 + t < len && tail0 + t > 0) p = cand_max(p, srow[tail0 + t]);
+    p = wave_max(p);
+    if (lane == 0) red[wv] = p;
+    if (t == 0) red[4] = nfull > 0 ? v[0].x : srow[0];  // the seed
+    __syncthreads();
+    p = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));  // -inf or >= +0: exact
+    const float cx = absmax_finish(red[4], p);
+    const float sc = inv_divide(range, cx);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int c = t + 256 * j;
+        if (c < nfull)
+            qrow[c] = pack4(quant_i8(v[j].x, sc), quant_i8(v[j].y, sc), quant_i8(v[j].z, sc), quant_i8(v[j].w, sc));
+    }
+    const int64_t first_zero = nfull + ((len & 3) ? 1 : 0);
+    if ((len & 3) && t == 0) {
+        int b[4] = {0, 0, 0, 0};
+        for (int e = 0; e < (len & 3); ++e) b[e] = quant_i8(srow[tail0 + e], sc);
+        qrow[nfull] = pack4(b[0], b[1], b[2], b[3]);
+    }
+    for (int64_t c = first_zero + t; c < nq; c += 256) qrow[c] = 0u;
+    if (t == 0) scale[row] = cx;
+}
+
+__global__ __launch_bounds__(256) void pack_rows_block_kernel(const float *__restrict__ src, int64_t sh, int rows,
+                                                              int len, float range, float *__restrict__ scale,
+                                                              int8_t *__restrict__ q, int64_t rows_pad,
+                                                              int64_t k_pad) {
+    __shared__ float red[8];
+    pack_row_block_body(blockIdx.x, src, sh, rows, len, range, scale, q, rows_pad, k_pad, red);
+}
+
 template <int R>
 __global__ __launch_bounds__(256) void pack_rows_vec_kernel(const float *__restrict__ src, int64_t sh, int rows,
                                                             int len, float range, float *__restrict__ scale,
@@ -230,6 +300,8 @@ __global__ __launch_bounds__(256) void pack_rows_and_colmax_kernel(
     const int bid = blockIdx.x;
     if (bid < ncol) {
         colmax_body<true>(bid % col_blocks, bid / col_blocks, b, bsh, k, n, b_partial, b_rows_pad, red);
+    } else if constexpr (R < 0) {
+        pack_row_block_body(bid - ncol, a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad, red);
     } else {
         pack_rows_vec_body<R>(bid - ncol, a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad);
     }
@@ -477,9 +549,10 @@ bool cols_vec_ok(const float *src, int64_t sh, int cols) {
     return (cols % 4 == 0) && (sh % 4 == 0) && (reinterpret_cast<uintptr_t>(src) % 16 == 0);
 }
 
-int rows_regs(int len) {  // float4 chunks per lane -> register-resident variant (0 = streaming)
+int rows_regs(int len) {  // float4 chunks per lane -> register-resident variant (-1 = block per row, 0 = streaming)
     const int per_lane = ((len >> 2) + 63) / 64;
-    return per_lane <= 1 ? 1 : per_lane <= 2 ? 2 : per_lane <= 4 ? 4 : per_lane <= 8 ? 8 : per_lane <= 16 ? 16 : 0;
+    if (per_lane > 16) return len <= kLongRowMax ? -1 : 0;
+    return per_lane <= 1 ? 1 : per_lane <= 2 ? 2 : per_lane <= 4 ? 4 : per_lane <= 8 ? 8 : 16;
 }
 
 }  // namespace
@@ -493,6 +566,11 @@ hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, 
         return hipGetLastError();
     }
 #define QG_ROWS(Rv) pack_rows_vec_kernel<Rv><<<grid, block, 0, stream>>>(src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad)
+    if (rows_regs(len) < 0) {
+        pack_rows_block_kernel<<<(unsigned)out.rows_pad, 256, 0, stream>>>(src, sh, rows, len, range, out.scale, out.q,
+                                                                           out.rows_pad, out.k_pad);
+        return hipGetLastError();
+    }
     switch (rows_regs(len)) {
         case 1: QG_ROWS(1); break;
         case 2: QG_ROWS(2); break;
@@ -557,13 +635,15 @@ hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k
     if (k < 2 || !rows_vec_ok(a, ash, 1, m) || !cols_vec_ok(b, bsh, n)) return hipErrorNotSupported;
     const int col_blocks = (n + kColBlock - 1) / kColBlock;
     const int ncol = col_blocks * (int)outb.parts;
-    const int nrow = (int)(outa.rows_pad / 4);
+    const int rr = rows_regs(k);
+    const int nrow = (int)(rr < 0 ? outa.rows_pad : outa.rows_pad / 4);  // block per row / 4 rows per block
 #define QG_FUSED(Rv)                                                                                            \
     pack_rows_and_colmax_kernel<Rv><<<ncol + nrow, 256, 0, stream>>>(a, ash, m, k, outa.scale, outa.q,          \
                                                                      outa.rows_pad, outa.k_pad, b, bsh, n,       \
                                                                      outb.scratch, outb.rows_pad, col_blocks,    \
                                                                      ncol, range)
-    switch (rows_regs(k)) {
+    switch (rr) {
+        case -1: QG_FUSED(-1); break;
         case 1: QG_FUSED(1); break;
         case 2: QG_FUSED(2); break;
         case 4: QG_FUSED(4); break;
