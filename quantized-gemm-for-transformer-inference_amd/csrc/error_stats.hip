@@ -65,7 +65,8 @@ __global__ __launch_bounds__(kStatThreads) void error_partials_kernel(const floa
 }
 
 __global__ __launch_bounds__(kStatThreads) void error_final_kernel(const Acc4 *__restrict__ partials, int nparts,
-                                                                   int64_t n, double *__restrict__ stats) {
+                                                                   int64_t n, int reference_order,
+                                                                   double *__restrict__ stats) {
     __shared__ Acc4 red[kStatThreads / 64];
     Acc4 v{0.0, 0.0, 0.0, 0.0};
     for (int i = threadIdx.x; i < nparts; i += kStatThreads) v = combine(v, partials[i]);
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(kStatThreads) void error_final_kernel(const Acc4 *_
         stats[2] = r.sum_abs / (double)n;
         stats[3] = r.max_abs;
         stats[4] = r.sum_ref / (double)n;
+        if (!reference_order) stats[0] = __builtin_nan("");  // not computed
     }
 }
 
@@ -128,14 +130,12 @@ hipError_t launch_error_stats(const float *C, const float *O, int64_t n, bool re
     int64_t want = (n + kStatThreads - 1) / kStatThreads;
     const int blocks = (int)(want < kStatBlocks ? (want > 0 ? want : 1) : kStatBlocks);
     error_partials_kernel<<<blocks, kStatThreads, 0, stream>>>(C, O, n, partials);
-    error_final_kernel<<<1, kStatThreads, 0, stream>>>(partials, blocks, n, stats);
+    error_final_kernel<<<1, kStatThreads, 0, stream>>>(partials, blocks, n, reference_order ? 1 : 0, stats);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (reference_order) {
         error_reference_mean_kernel<<<1, 64, 0, stream>>>(C, O, n, stats);
         e = hipGetLastError();
-    } else {
-        e = hipMemsetAsync(stats, 0xff, sizeof(double), stream);  // stats[0] = NaN: not computed
     }
     return e;
 }

@@ -76,6 +76,14 @@ size_t gemm_scratch_bytes(int m, int n, int k) {
     return ticket_bytes(tiles) + (size_t)tiles * g.splits * g.tile * g.tile * 4;
 }
 
+// zeroes the ticket region ahead of a split launch.  A kernel rather than hipMemsetAsync: inside a
+// captured HIP graph the memset node left the tickets unzeroed on replay (every slice then saw a
+// nonzero ticket and no tile was written) -- a kernel node replays as launched.
+__global__ __launch_bounds__(256) void zero_tickets_kernel(unsigned *__restrict__ t, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) t[i] = 0u;
+}
+
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     const GemmEvents ev = take_gemm_events();
@@ -117,10 +125,12 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
         p.splits = g.splits;
         p.tickets = static_cast<unsigned *>(scratch);
         p.slabs = reinterpret_cast<int32_t *>(static_cast<char *>(scratch) + ticket_bytes(tiles));
-        // the tickets are polled state: zeroed ahead of every launch (a memset node under capture) unless
-        // the scratch is library-owned, zeroed at allocation and re-zeroed by each launch's reducers
+        // the tickets are polled state: zeroed ahead of every launch unless the scratch is
+        // library-owned, zeroed at allocation and re-zeroed by each launch's reducers
         if (!tickets_zeroed) {
-            hipError_t e = hipMemsetAsync(p.tickets, 0, ticket_bytes(tiles), stream);
+            const int nt = (int)(ticket_bytes(tiles) / sizeof(unsigned));
+            zero_tickets_kernel<<<(nt + 255) / 256, 256, 0, stream>>>(p.tickets, nt);
+            hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
     }

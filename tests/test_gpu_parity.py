@@ -235,3 +235,48 @@ def test_harness_binary_reproduces_reference_output(qg):
     e = lines.index("Mean quantization error:")
     assert abs(float(lines[e + 1]) - 0.003937006) < 1e-8
     assert "All tests completed successfully!" in lines
+
+
+def test_hip_graph_capture_replays_bit_exact(qg, oracle, device):
+    """op_mm_quantize_ws with a caller workspace makes no allocation and no host sync, so it can be
+    captured in a HIP graph (torch.cuda.CUDAGraph) and replayed; split-K shapes included (their ticket
+    memset is a graph node)."""
+    L = qg.load()
+    for (M, N, K) in [(384, 512, 640), (512, 1024, 4096)]:
+        X, W = oracle.inputs(M, N, K, 111)
+        want = oracle.quantized_mm(X, W)
+        Xd, Wd = _dev(X, device), _dev(W, device)
+        ws = torch.empty(L.op_mm_quantize_workspace_size(M, N, K), dtype=torch.uint8, device=device)
+        O = torch.full((M, N), float("nan"), device=device)
+        s = torch.cuda.Stream(device)
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                rc = L.op_mm_quantize_ws(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, 127.0,
+                                         ws.data_ptr(), ws.numel(), s.cuda_stream)
+                assert rc == 0
+        for _ in range(3):
+            O.fill_(float("nan"))
+            g.replay()
+            torch.cuda.synchronize()
+            assert_bits_equal(O.cpu().numpy(), want, f"graph replay {M}x{N}x{K}")
+
+
+def test_concurrent_streams_with_own_workspaces(qg, oracle, device):
+    L = qg.load()
+    M, N, K = 512, 1024, 4096  # split-K plan on both streams
+    cases = []
+    for i in range(2):
+        X, W = oracle.inputs(M, N, K, 120 + i)
+        cases.append((_dev(X, device), _dev(W, device), oracle.quantized_mm(X, W),
+                      torch.empty(L.op_mm_quantize_workspace_size(M, N, K), dtype=torch.uint8, device=device),
+                      torch.empty((M, N), device=device), torch.cuda.Stream(device)))
+    torch.cuda.synchronize()
+    for _ in range(5):
+        for Xd, Wd, _, ws, O, s in cases:
+            rc = L.op_mm_quantize_ws(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, 127.0,
+                                     ws.data_ptr(), ws.numel(), s.cuda_stream)
+            assert rc == 0
+    torch.cuda.synchronize()
+    for i, (_, _, want, _, O, _) in enumerate(cases):
+        assert_bits_equal(O.cpu().numpy(), want, f"stream {i}")
