@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes over the encoder forward probe (kernel dispatch counters only, one counter group per pass).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc_encoder; mkdir -p $OUT
+i=0
+for P in "FETCH_SIZE" "WRITE_SIZE" \
+         "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" \
+         "TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $OUT -o pass$i -- python3 scripts/encoder_probe.py > $OUT/pass$i.log 2>&1
+  rc=$?; echo "pass$i ($P) rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+echo done

@@ -194,11 +194,45 @@ def test_explicit_workspace_and_prepacked_weights(qg, oracle, device):
 
 
 def test_unquantized_gemm_matches_reference_order(qg, oracle, device):
-    """qgemm_mm_fp32 is the reference's op_mm<float,float>: sequential-k fmaf, bit-exact."""
-    for M, N, K in [(100, 70, 96), (33, 65, 130)]:
+    """qgemm_mm_fp32 is the reference's op_mm<float,float>: sequential-k fmaf, bit-exact (on the f32
+    MFMA: every tile configuration, k % 4 / k % 32 tails, K = 1)."""
+    for M, N, K in [(100, 70, 96), (33, 65, 130), (512, 512, 64), (257, 300, 1000), (1, 77, 33), (64, 1, 5),
+                    (5, 3, 1), (640, 640, 128), (2048, 1024, 64)]:
         X, W = oracle.inputs(M, N, K, 61)
         C = qg.mm_fp32(_dev(X, device), _dev(W, device)).cpu().numpy()
         assert_bits_equal(C, oracle.mm_fp32(X, W), f"fp32 {M}x{N}x{K}")
+
+
+def test_unquantized_gemm_strided_views(qg, oracle, device):
+    """Column-major / transposed operand views (the attention Q K^T form) stage through the other LDS
+    layout; same bits as the contiguous oracle on the same logical matrices."""
+    M, N, K = 192, 160, 200
+    X, W = oracle.inputs(M, N, K, 62)
+    want = oracle.mm_fp32(X, W)
+    Xc = _dev(np.ascontiguousarray(X.T), device).t()  # stride (1, M)
+    Wc = _dev(np.ascontiguousarray(W.T), device).t()  # stride (1, K)
+    for a, b, what in [(Xc, _dev(W, device), "A col-major"), (_dev(X, device), Wc, "B col-major"), (Xc, Wc, "both")]:
+        assert_bits_equal(qg.mm_fp32(a, b).cpu().numpy(), want, f"fp32 views: {what}")
+
+
+def test_unquantized_gemm_special_values(qg, oracle, device):
+    """Underflowing products (-0 and subnormal results), +-inf and NaN operands: the MFMA chain keeps
+    the fmaf chain's bits (subnormals are not flushed; a -0 result becomes +0 only through the
+    reference's zero-padded tail)."""
+    rng = np.random.default_rng(63)
+    for M, N, K in [(48, 40, 64), (48, 40, 36), (40, 48, 7)]:
+        X = (rng.uniform(-1, 1, (M, K)) * 1e-20).astype(np.float32)
+        W = (rng.uniform(-1, 1, (K, N)) * 1e-20).astype(np.float32)
+        W[:, :8] *= np.float32(1e-6)   # products far below the smallest subnormal: signed zeros
+        X[:4, :] *= np.float32(1e19)   # some rows land in the subnormal range
+        X[5, 3] = np.inf
+        X[6, 2] = -np.inf
+        W[1, 9] = np.nan
+        W[2, 11] = np.inf
+        want = oracle.mm_fp32(X, W)
+        got = qg.mm_fp32(_dev(X, device), _dev(W, device)).cpu().numpy()
+        assert_bits_equal(got, want, f"fp32 special {M}x{N}x{K}")
+        assert (np.signbit(want) & (want == 0)).any() or K % 32, "case should produce -0 results"
 
 
 def test_device_error_stats_match_oracle(qg, oracle, device):
