@@ -227,7 +227,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs &p, int8_t *lds, v16i (&
     }
 }
 
-enum V2Flags { kPrio = 1, kNoGlds = 2, kNoLdsRead = 4, kNoBarrier = 8, kNoVmWait = 16 };
+enum V2Flags { kPrio = 1, kNoGlds = 2, kNoLdsRead = 4, kNoBarrier = 8, kNoVmWait = 16, kNoSlab = 32 /* lab ablation */ };
 
 // ------------------------------------------------------------------------------------------------
 // v1: stage(kt+1) ; compute(kt) with just-in-time fragment reads ; vmcnt(0) ; barrier
@@ -394,7 +394,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 // draws the ticket with a relaxed agent-scope add -- no release fence (a buffer_wbl2 would also write
 // back every dirty line of the XCD's L2, including other blocks' output tiles); the reducer reads
 // the other slabs with sc1 loads (every load of them), so no acquire either.
-template <int MI, int NI, int kWaves>
+template <int MI, int NI, int kWaves, bool kSlab = true>
 __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last, v4i (&acc)[MI][NI], int tile,
                                                int slice, int S, int wave, int lane, int tid) {
     constexpr int kSlabBytes = kWaves * MI * NI * 64 * 16;
@@ -406,7 +406,7 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-            __builtin_amdgcn_raw_buffer_store_b128(acc[mi][ni], rsrc, slice * kSlabBytes + lane_off + (mi * NI + ni) * 1024,
+            if constexpr (kSlab) __builtin_amdgcn_raw_buffer_store_b128(acc[mi][ni], rsrc, slice * kSlabBytes + lane_off + (mi * NI + ni) * 1024,
                                                    0, 16 /* sc1 */);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -421,7 +421,7 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last
     if (*last != (unsigned)(S - 1)) return false;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: loads stay below
     for (int s = 0; s < S; ++s) {
-        if (s == slice) continue;
+        if (s == slice || !kSlab) continue;
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -501,7 +501,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
     }
 
     if (S > 1 &&
-        !splitk_combine<8, 4, 8>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice, S, wave, lane, tid))
+        !splitk_combine<8, 4, 8, !(kFlags & kNoSlab)>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice,
+                                                     S, wave, lane, tid))
         return;
     epilogue16<kMode, kEpi>(p, lds, acc, tm, tn, wm, wn, lane, tid);
 }

@@ -32,8 +32,50 @@ __global__ void to_tiled(const int8_t *src, int8_t *dst, int64_t rows, int64_t k
     }
 }
 
+
+// peak mode: bare v_mfma_i32_16x16x64_i8 issue, operands in registers (8 A x 4 B fragments, 32
+// independent accumulators = the product kernel's wave tile), 512-thread blocks (2 waves/SIMD), one
+// block per CU; every iteration XORs a new pattern into the operands so their bits keep toggling as on
+// random data.  Per-block stamps give the in-kernel clock.
+__global__ __launch_bounds__(512, 1) void mfma_peak(int iters, uint64_t seed, int *out, unsigned long long *stamp) {
+    const int tid = threadIdx.x;
+    if (tid == 0) { stamp[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime(); stamp[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime(); }
+    v4i a[8], b[4], acc[8][4];
+    uint64_t z = mix64(seed + blockIdx.x * 512 + tid);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { z = mix64(z); a[i] = v4i{(int)z, (int)(z >> 32), (int)(z * 3), (int)(z >> 17)}; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { z = mix64(z); b[i] = v4i{(int)z, (int)(z >> 32), (int)(z * 5), (int)(z >> 13)}; }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4i{};
+    unsigned pat = (unsigned)z | 0x01010101u;
+    for (int it = 0; it < iters; ++it) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pat = pat * 1664525u + 1013904223u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] ^= (int)pat;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] ^= (int)(pat >> 3);
+    }
+    int x = 0;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) x ^= acc[mi][ni][0] ^ acc[mi][ni][1] ^ acc[mi][ni][2] ^ acc[mi][ni][3];
+    out[blockIdx.x * 512 + tid] = x;
+    if (tid == 0) { stamp[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime(); stamp[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime(); }
+}
+
 typedef void (*KernelFn)(GemmArgs);
-struct Variant { const char *name; KernelFn fn; bool check; bool tiled = false; int threads = kThreads; };
+struct Variant { const char *name; KernelFn fn; bool check; bool tiled = false; int threads = kThreads; int grid = 0; };
 
 int main(int argc, char **argv) {
     int m = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 4096;
@@ -133,10 +175,91 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
+    // peak mode: build/gemm_lab 256 256 128 0 peak (sizes unused)
+    if (only && std::string(only) == "peak") {
+        int *out; unsigned long long *st;
+        const int nb = 256, iters = 4096;
+        CK(hipMalloc(&out, nb * 512 * 4)); CK(hipMalloc(&st, nb * 4 * 8));
+        hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
+        int launches = 0; float ms = 0;
+        CK(hipEventRecord(a));
+        while (ms < 2000) {
+            for (int i = 0; i < 20; ++i) mfma_peak<<<nb, 512>>>(iters, 7 + launches + i, out, st);
+            launches += 20;
+            CK(hipEventRecord(z)); CK(hipEventSynchronize(z)); CK(hipEventElapsedTime(&ms, a, z));
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned long long> h((size_t)nb * 4);
+        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<double> clk;
+        for (int i = 0; i < nb; ++i) clk.push_back((double)(h[i * 4 + 2] - h[i * 4]) / (double)(h[i * 4 + 3] - h[i * 4 + 1]) * 0.1);
+        std::sort(clk.begin(), clk.end());
+        const double ops = 2.0 * 16 * 16 * 64 * 32 * (double)iters * 8 * nb;  // per launch
+        const double us = ms * 1000 / launches;
+        printf("mfma_peak: %.1f us per launch, %.1f TOPS (%.1f%% of 5033), in-kernel clock median %.3f GHz (min %.3f max %.3f); "
+               "at that clock the pipe peak is %.1f TOPS\n", us, ops / us * 1e-6, ops / us * 1e-6 / 50.332, clk[nb / 2], clk[0],
+               clk[nb - 1], 256.0 * 4 * 2048 * clk[nb / 2] * 1e-3);
+        return 0;
+    }
+    // split mode: build/gemm_lab m n k rounds split -- the product kernel at split-K S = 1, 2, 4 (and the
+    // slab-free ablation: tickets only, wrong sums) on library-style scratch (tickets zeroed once,
+    // reducers re-zero them), interleaved rounds
+    if (only && std::string(only) == "split") {
+        const int tiles = p.tiles_m * p.tiles_n;
+        unsigned *tick; int32_t *slabs;
+        CK(hipMalloc(&tick, 4096)); CK(hipMemset(tick, 0, 4096));
+        CK(hipMalloc(&slabs, (size_t)tiles * 8 * BM * BN * 4));
+        struct SV { const char *name; KernelFn fn; int S; };
+        std::vector<SV> sv = {
+            {"S1", gemm_i8_v3<kStoreLds, true, kPrio>, 1},
+            {"S2", gemm_i8_v3<kStoreLds, true, kPrio>, 2},
+            {"S2_noslab", gemm_i8_v3<kStoreLds, true, kPrio | kNoSlab>, 2},
+            {"S4", gemm_i8_v3<kStoreLds, true, kPrio>, 4},
+            {"S4_noslab", gemm_i8_v3<kStoreLds, true, kPrio | kNoSlab>, 4},
+        };
+        auto args = [&](int S, float *out) {
+            GemmArgs q = p; q.C = out; q.splits = S; q.slabs = slabs; q.tickets = tick; q.reset_tickets = 1;
+            return q;
+        };
+        std::vector<float> h1((size_t)m * n), h2((size_t)m * n);
+        sv[0].fn<<<dim3(tiles), dim3(kThreads)>>>(args(1, Cref));
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h1.data(), Cref, h1.size() * 4, hipMemcpyDeviceToHost));
+        for (auto &v : sv) {
+            if (std::string(v.name).find("noslab") != std::string::npos) continue;
+            CK(hipMemset(C, 0xff, (size_t)m * n * 4));
+            v.fn<<<dim3(tiles * v.S), dim3(kThreads)>>>(args(v.S, C));
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(h2.data(), C, h2.size() * 4, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t i = 0; i < h1.size(); ++i) bad += memcmp(&h1[i], &h2[i], 4) != 0;
+            printf("check %-10s mismatches %zu\n", v.name, bad);
+        }
+        hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        std::vector<std::vector<float>> t(sv.size());
+        for (int r = 0; r < std::max(rounds, 3); ++r)
+            for (size_t vi = 0; vi < sv.size(); ++vi) {
+                const GemmArgs q = args(sv[vi].S, C);
+                const dim3 g(tiles * sv[vi].S);
+                for (int w = 0; w < 3; ++w) sv[vi].fn<<<g, dim3(kThreads)>>>(q);
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < reps; ++i) sv[vi].fn<<<g, dim3(kThreads)>>>(q);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                t[vi].push_back(ms * 1000 / reps);
+            }
+        for (size_t vi = 0; vi < sv.size(); ++vi) {
+            auto v = t[vi]; std::sort(v.begin(), v.end());
+            printf("%-10s median %8.2f us  min %8.2f us\n", sv[vi].name, v[v.size() / 2], v[0]);
+        }
+        return 0;
+    }
     if (only) {
         std::vector<Variant> keep;
+        const std::string list = std::string(",") + only + ",";  // comma-separated names
         for (auto &v : vs)
-            if (std::string(v.name) == only || std::string(v.name) == "v1_direct") keep.push_back(v);
+            if (list.find(std::string(",") + v.name + ",") != std::string::npos || std::string(v.name) == "v1_direct")
+                keep.push_back(v);
         vs = keep;
     }
     dim3 grid(p.tiles_m * p.tiles_n), block(kThreads);
@@ -149,7 +272,7 @@ int main(int argc, char **argv) {
     for (auto &v : vs) {
         if (!v.check) continue;
         CK(hipMemset(C, 0xff, (size_t)m * n * 4));
-        v.fn<<<grid, dim3(v.threads)>>>(v.tiled ? pt : p);
+        v.fn<<<v.grid ? dim3(v.grid) : grid, dim3(v.threads)>>>(v.tiled ? pt : p);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
         size_t bad = 0;
@@ -161,9 +284,9 @@ int main(int argc, char **argv) {
     for (int r = 0; r < rounds; ++r)
         for (size_t vi = 0; vi < vs.size(); ++vi) {
             const GemmArgs &pp = vs[vi].tiled ? pt : p;
-            for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, dim3(vs[vi].threads)>>>(pp);
+            for (int w = 0; w < 3; ++w) vs[vi].fn<<<vs[vi].grid ? dim3(vs[vi].grid) : grid, dim3(vs[vi].threads)>>>(pp);
             CK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, dim3(vs[vi].threads)>>>(pp);
+            for (int i = 0; i < reps; ++i) vs[vi].fn<<<vs[vi].grid ? dim3(vs[vi].grid) : grid, dim3(vs[vi].threads)>>>(pp);
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             t[vi].push_back(ms * 1000 / reps);
