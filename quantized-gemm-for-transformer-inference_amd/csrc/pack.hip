@@ -529,6 +529,127 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Single pass at TWO blocks per CU (K <= 4096, n % 8 == 0): 512-thread blocks with the same 16 float4
+// per thread, so a block fits in 88 VGPRs (5 waves/SIMD) and a second block on the CU streams its
+// loads while the first reduces, quantizes and stores (the 1024-thread single pass leaves the CU's HBM
+// stream idle through those phases).  Roles:
+//   W strip (blocks [0, n/8)): 8 columns x all K rows; thread t: c2 = t & 1 (columns n0 + 4*c2 .. +3),
+//       rows 4*(t>>1) + e + 1024*i (e, i = 0..3).  One wave instruction reads 32 rows x 32 B; the four
+//       strips sharing a 128-B line of W run on one XCD (blocks b, b+8, b+16, b+24 get adjacent strips)
+//       so the line is fetched once.  Loads and stores are buffer instructions on a wave-uniform
+//       descriptor with ONE per-lane offset; rows >= K lie past the descriptor and read as zeros.
+//   X rows (the rest): 8 rows per block, one wave per row (pack_rows_vec_body<16>).
+// Measured (lab/pack2_lab.hip, 4096^3): 28.0 us vs 31.7 us for the 16-column single pass; better up to
+// n = 8192 at K >= 2048, worse for wider W (n = 12288, 16384) and short K, where the 16-column pass stays.
+constexpr int kWs8Cols = 8;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
+                                                   float range, float *__restrict__ scale, int8_t *__restrict__ q,
+                                                   int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */) {
+    typedef int v4i_t __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int c2 = t & 1, rq = t >> 1;
+    const int64_t n0 = (int64_t)strip * kWs8Cols;
+    const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kWs8Cols) * 4));
+    const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c2) * 4);
+    float4 v[4][4];  // [i][e]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, 0);
+            v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
+        }
+    // column candidates over rows >= 1 (row 0 is the seed)
+    float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 1024 * i;
+            if (r >= 1 && r < k) {
+                p0 = cand_max(p0, v[i][e].x);
+                p1 = cand_max(p1, v[i][e].y);
+                p2 = cand_max(p2, v[i][e].z);
+                p3 = cand_max(p3, v[i][e].w);
+            }
+        }
+    // over the 32 lanes of the wave with the same c2 (lane bits 1..5), then over the 8 waves
+#pragma unroll
+    for (int off = 2; off < 64; off <<= 1) {
+        p0 = fmaxf(p0, __shfl_xor(p0, off, 64));
+        p1 = fmaxf(p1, __shfl_xor(p1, off, 64));
+        p2 = fmaxf(p2, __shfl_xor(p2, off, 64));
+        p3 = fmaxf(p3, __shfl_xor(p3, off, 64));
+    }
+    if (lane < 2) {
+        red[wv * 8 + 4 * lane + 0] = p0;
+        red[wv * 8 + 4 * lane + 1] = p1;
+        red[wv * 8 + 4 * lane + 2] = p2;
+        red[wv * 8 + 4 * lane + 3] = p3;
+    }
+    __syncthreads();
+    float *s_sh = red + 8 * 8;
+    if (t < kWs8Cols) {
+        float pm = red[t];
+#pragma unroll
+        for (int ww = 1; ww < 8; ++ww) pm = fmaxf(pm, red[ww * 8 + t]);  // -inf or >= +0: exact
+        const float cw = absmax_finish(w[n0 + t], pm);                  // seed = W[0, j]
+        s_sh[t] = inv_divide(range, cw);
+        scale[n0 + t] = cw;
+    }
+    __syncthreads();
+    const float s0 = s_sh[4 * c2 + 0], s1 = s_sh[4 * c2 + 1], s2 = s_sh[4 * c2 + 2], s3 = s_sh[4 * c2 + 3];
+    // 4 consecutive rows of one column = one dword of packed row n0 + 4*c2 + cc
+    const auto dst = buf_rsrc(q + n0 * k_pad, (uint32_t)(kWs8Cols * k_pad));
+    const uint32_t vq = (uint32_t)(4 * c2 * k_pad + 4 * rq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r0 = 4 * rq + 1024 * i;
+        if (r0 >= k_pad) continue;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            int qe[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = cc == 0 ? v[i][e].x : cc == 1 ? v[i][e].y : cc == 2 ? v[i][e].z : v[i][e].w;
+                const float sc = cc == 0 ? s0 : cc == 1 ? s1 : cc == 2 ? s2 : s3;
+                qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
+            }
+            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst, vq,
+                                                  (uint32_t)(cc * k_pad + 1024 * i), 0);
+        }
+    }
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 5))) void pack_single_pass8_kernel(
+    const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
+    int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
+    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range) {
+    __shared__ float red[8 * 8 + 8];
+    const int bid = blockIdx.x;
+    const int npad = (int)((w_rows_pad - n) / kWs8Cols);
+    if (bid < nstrips) {
+        // blocks b, b+8, ... run on one XCD: XCD-contiguous strip ranges (bijective for any nstrips)
+        const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
+        const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        pack_w_strip8_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, red);
+    } else if (bid < nstrips + npad) {
+        const int64_t n0 = n + (int64_t)(bid - nstrips) * kWs8Cols;
+        for (int64_t i = threadIdx.x; i < (int64_t)kWs8Cols * k_pad / 16; i += 512)
+            reinterpret_cast<uint4 *>(w_q + n0 * k_pad)[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x < kWs8Cols) w_scale[n0 + threadIdx.x] = 0.0f;
+    } else {
+        const int64_t xb = bid - nstrips - npad;  // rows 8xb + (t>>6): two 4-row groups of the 256-thread body
+        pack_rows_vec_body<16>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void fill_uniform_kernel(float *__restrict__ dst, int64_t count, uint64_t seed,
                                                            float lo, float hi) {
     const uint64_t key = mix64(seed + 0x9E3779B97F4A7C15ULL);
@@ -608,10 +729,26 @@ hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, flo
     return launch_pack_cols_pass2(src, sh, len, cols, range, out, stream);
 }
 
-hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream) {
-    if (k < 1 || k > kWsMaxK || n % kWsCols != 0 || !rows_vec_ok(x, xsh, 1, m) || !cols_vec_ok(w, wsh, n))
-        return hipErrorNotSupported;
+// kind: 0 = choose (the 8-column two-blocks-per-CU pass where it measured faster, else 16 columns),
+// 8 or 16 = force that strip width (lab)
+hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
+                                        int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind) {
+    if (k < 1 || k > kWsMaxK || !rows_vec_ok(x, xsh, 1, m) || !cols_vec_ok(w, wsh, n)) return hipErrorNotSupported;
+    const bool can8 = n % kWs8Cols == 0 && ((int64_t)k * wsh + kWs8Cols) * 4 < ((int64_t)1 << 31);
+    const bool can16 = n % kWsCols == 0;
+    if (kind == 0) kind = (can8 && n <= 8192 && k > 1024) || !can16 ? 8 : 16;
+    if (kind == 8) {
+        if (!can8) return hipErrorNotSupported;
+        const int nstrips = n / kWs8Cols;
+        const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
+        const int nx = (int)(outx.rows_pad / 8);
+        pack_single_pass8_kernel<<<nstrips + npad + nx, 512, 0, stream>>>(x, xsh, m, k, outx.scale, outx.q,
+                                                                          outx.rows_pad, outx.k_pad, w, wsh, n,
+                                                                          outw.scale, outw.q, outw.rows_pad, nstrips,
+                                                                          range);
+        return hipGetLastError();
+    }
+    if (!can16) return hipErrorNotSupported;
     const int nstrips = n / kWsCols;
     const int npad = (int)((outw.rows_pad - n) / kWsCols);
     const int nx = (int)(outx.rows_pad / 16);
@@ -620,6 +757,11 @@ hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, Pa
                                                                          outx.k_pad, w, wsh, n, outw.scale, outw.q,
                                                                          outw.rows_pad, nstrips, range);
     return hipGetLastError();
+}
+
+hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
+                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream) {
+    return launch_pack_single_pass_kind(x, xsh, m, k, outx, w, wsh, n, outw, range, stream, 0);
 }
 
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream) {

@@ -94,10 +94,14 @@ hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, flo
 // Returns hipErrorNotSupported when the layouts do not allow it (caller falls back).
 hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,
                                        int64_t bsh, int n, PackedView outb, float range, hipStream_t stream);
-// One launch, W read once: single-pass W strips (K <= 4096, n % 16 == 0) + X rows.  hipErrorNotSupported
-// when the shape/layout is outside that (caller falls back).
+// One launch, W read once: single-pass W strips (K <= 4096, n % 8 == 0: 8-column strips at two blocks
+// per CU, or 16-column strips) + X rows.  hipErrorNotSupported when the shape/layout is outside that
+// (caller falls back).
 hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
                                    int64_t wsh, int n, PackedView outw, float range, hipStream_t stream);
+// kind 8 / 16 forces the strip width (lab); 0 chooses.
+hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
+                                        int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind);
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);

@@ -84,6 +84,20 @@ def test_random_shapes_full_oracle(qg, oracle, device, M, N, K):
     assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N,K", [(130, 264, 1500), (70, 200, 600), (300, 4104, 4096), (96, 8192, 1025),
+                                   (1, 8, 2), (33, 24, 4096), (257, 1032, 3000)])
+def test_single_pass_8_column_strips(qg, oracle, device, M, N, K):
+    """Shapes on the single-pass pack with 8-column W strips (n % 8 == 0 and n <= 8192 with K > 1024,
+    or n % 16 != 0): buffer loads past the last row read zeros, padding strips, odd strip counts over
+    the XCD map; W columns whose signed first element is the largest magnitude (absmax seed quirk)."""
+    X, W = oracle.inputs(M, N, K, 61)
+    W[0, ::3] = -1.75  # seed quirk in every third column (int8 saturation on the quantize)
+    X[::5, 0] = -1.5
+    O, ref = oracle.quantized_mm(X, W, intermediates=True)
+    assert_bits_equal(_run_full(qg, X, W, device), O, f"{M}x{N}x{K}")
+    _check_intermediates(qg, X, W, ref, device, f"{M}x{N}x{K}")
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 4096), (300, 520, 1000), (512, 1024, 2048)])
 def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
     """Few-tile shapes run split-K (int32 slabs + arrival tickets, combined in-launch): exact integer
