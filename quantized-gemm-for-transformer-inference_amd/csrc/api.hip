@@ -179,19 +179,25 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     char *pa = scratch + align256(sb);
     char *pb = pa + align256(packed_bytes(m, k));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    auto gemm = [&]() { return err(mm_packed_impl(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s)); };
+    auto gemm = [&](bool tickets_zeroed) {
+        return err(mm_packed_impl(pa, pb, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s, tickets_zeroed));
+    };
+    // the pack launch zeroes the split-K tickets at the start of the workspace (the GEMM then needs no
+    // zeroing launch of its own)
+    uint32_t *tickets = reinterpret_cast<uint32_t *>(scratch);
+    const int ntickets = (int)(gemm_ticket_bytes(m, n, k) / 4);
     // Common case (row-major X and W): X's row pass and W's column-absmax pass share one launch,
     // then W's quantize/transpose pass, then the GEMM -- three launches in all.
     if (a_stride_w == 1 && b_stride_w == 1 && k > 1) {
         const PackedView va = packed_view(pa, m, k), vb = packed_view(pb, n, k);
         // K <= 4096: W read once (single-pass strips) -- two launches in all
-        hipError_t e = launch_pack_single_pass(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
-        if (e == hipSuccess) return gemm();
+        hipError_t e = launch_pack_single_pass(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s, tickets, ntickets);
+        if (e == hipSuccess) return gemm(true);
         if (e != hipErrorNotSupported) return err(e);
-        e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s);
+        e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s, tickets, ntickets);
         if (e == hipSuccess) {
             if ((e = launch_pack_cols_pass2(B, b_stride_h, k, n, range, vb, s)) != hipSuccess) return err(e);
-            return gemm();
+            return gemm(true);
         }
         if (e != hipErrorNotSupported) return err(e);
     }
@@ -199,7 +205,7 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     if (rc) return rc;
     rc = qgemm_pack_b(B, b_stride_h, b_stride_w, k, n, range, pb, stream);
     if (rc) return rc;
-    return gemm();
+    return gemm(false);
 }
 
 int op_mm_quantize_ex(const float *A, int64_t a_stride_h, int64_t a_stride_w, const float *B, int64_t b_stride_h,

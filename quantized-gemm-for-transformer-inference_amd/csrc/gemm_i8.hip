@@ -69,6 +69,8 @@ static size_t ticket_bytes(int64_t tiles) {
     return kTicketBytes;
 }
 
+size_t gemm_ticket_bytes(int m, int n, int k) { return gemm_plan(m, n, k).splits > 1 ? kTicketBytes : 0; }
+
 size_t gemm_scratch_bytes(int m, int n, int k) {
     const GemmPlan g = gemm_plan(m, n, k);
     if (g.splits <= 1) return 0;

@@ -47,6 +47,14 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+// The GEMM's split-K tickets live in the caller's workspace, whose contents are arbitrary: the pack
+// launch that precedes the GEMM in the same stream zeroes them (block 0), which saves the GEMM a
+// zeroing launch of its own.
+__device__ __forceinline__ void zero_words_block0(uint32_t *words, int n) {
+    if (n > 0 && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < n; i += blockDim.x) words[i] = 0u;
+}
+
 // ------------------------------------------------------------------------------------------------
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
 // R > 0: each lane keeps R float4 chunks in registers (len <= 256*R), one HBM read.
@@ -295,9 +303,11 @@ template <int R>
 __global__ __launch_bounds__(256) void pack_rows_and_colmax_kernel(
     const float *__restrict__ a, int64_t ash, int m, int k, float *__restrict__ a_scale, int8_t *__restrict__ a_q,
     int64_t a_rows_pad, int64_t k_pad, const float *__restrict__ b, int64_t bsh, int n,
-    uint32_t *__restrict__ b_partial, int64_t b_rows_pad, int col_blocks, int ncol, float range) {
+    uint32_t *__restrict__ b_partial, int64_t b_rows_pad, int col_blocks, int ncol, float range, uint32_t *zero_words,
+    int nzero) {
     __shared__ float red[4 * 256];
     const int bid = blockIdx.x;
+    zero_words_block0(zero_words, nzero);
     if (bid < ncol) {
         colmax_body<true>(bid % col_blocks, bid / col_blocks, b, bsh, k, n, b_partial, b_rows_pad, red);
     } else if constexpr (R < 0) {
@@ -504,8 +514,9 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
 __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
-    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range) {
+    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    zero_words_block0(zero_words, nzero);
     // roles by block id: [W strips][zero padding strips][X rows] (lab, 4096^3: 30.4 us; X rows first
     // 31.5 us; W and X interleaved in groups of 8 blocks 35.1 us)
     const int bid = blockIdx.x;
@@ -629,9 +640,10 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 5))) void pack_single_pass8_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
-    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range) {
+    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero) {
     __shared__ float red[8 * 8 + 8];
     const int bid = blockIdx.x;
+    zero_words_block0(zero_words, nzero);
     const int npad = (int)((w_rows_pad - n) / kWs8Cols);
     if (bid < nstrips) {
         // blocks b, b+8, ... run on one XCD: XCD-contiguous strip ranges (bijective for any nstrips)
@@ -732,7 +744,8 @@ hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, flo
 // kind: 0 = choose (the 8-column two-blocks-per-CU pass where it measured faster, else 16 columns),
 // 8 or 16 = force that strip width (lab)
 hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                        int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind) {
+                                        int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind,
+                                        uint32_t *zero_words, int nzero) {
     if (k < 1 || k > kWsMaxK || !rows_vec_ok(x, xsh, 1, m) || !cols_vec_ok(w, wsh, n)) return hipErrorNotSupported;
     const bool can8 = n % kWs8Cols == 0 && ((int64_t)k * wsh + kWs8Cols) * 4 < ((int64_t)1 << 31);
     const bool can16 = n % kWsCols == 0;
@@ -745,7 +758,7 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
         pack_single_pass8_kernel<<<nstrips + npad + nx, 512, 0, stream>>>(x, xsh, m, k, outx.scale, outx.q,
                                                                           outx.rows_pad, outx.k_pad, w, wsh, n,
                                                                           outw.scale, outw.q, outw.rows_pad, nstrips,
-                                                                          range);
+                                                                          range, zero_words, nzero);
         return hipGetLastError();
     }
     if (!can16) return hipErrorNotSupported;
@@ -755,13 +768,15 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
     const size_t lds = 4096;  // [16 waves][16 cols] partial maxima + 16 scales
     pack_single_pass_kernel<<<nstrips + npad + nx, 1024, lds, stream>>>(x, xsh, m, k, outx.scale, outx.q, outx.rows_pad,
                                                                          outx.k_pad, w, wsh, n, outw.scale, outw.q,
-                                                                         outw.rows_pad, nstrips, range);
+                                                                         outw.rows_pad, nstrips, range, zero_words,
+                                                                         nzero);
     return hipGetLastError();
 }
 
 hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream) {
-    return launch_pack_single_pass_kind(x, xsh, m, k, outx, w, wsh, n, outw, range, stream, 0);
+                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream,
+                                   uint32_t *zero_words, int nzero) {
+    return launch_pack_single_pass_kind(x, xsh, m, k, outx, w, wsh, n, outw, range, stream, 0, zero_words, nzero);
 }
 
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream) {
@@ -773,7 +788,8 @@ hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float l
 }
 
 hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,
-                                         int64_t bsh, int n, PackedView outb, float range, hipStream_t stream) {
+                                         int64_t bsh, int n, PackedView outb, float range, hipStream_t stream,
+                                         uint32_t *zero_words, int nzero) {
     if (k < 2 || !rows_vec_ok(a, ash, 1, m) || !cols_vec_ok(b, bsh, n)) return hipErrorNotSupported;
     const int col_blocks = (n + kColBlock - 1) / kColBlock;
     const int ncol = col_blocks * (int)outb.parts;
@@ -783,7 +799,7 @@ hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k
     pack_rows_and_colmax_kernel<Rv><<<ncol + nrow, 256, 0, stream>>>(a, ash, m, k, outa.scale, outa.q,          \
                                                                      outa.rows_pad, outa.k_pad, b, bsh, n,       \
                                                                      outb.scratch, outb.rows_pad, col_blocks,    \
-                                                                     ncol, range)
+                                                                     ncol, range, zero_words, nzero)
     switch (rr) {
         case -1: QG_FUSED(-1); break;
         case 1: QG_FUSED(1); break;

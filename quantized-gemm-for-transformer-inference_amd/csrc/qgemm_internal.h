@@ -93,15 +93,19 @@ hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, flo
 // One launch: pack_rows of a row-major A (vector path) and pass 1 of pack_cols of a row-major B.
 // Returns hipErrorNotSupported when the layouts do not allow it (caller falls back).
 hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,
-                                       int64_t bsh, int n, PackedView outb, float range, hipStream_t stream);
+                                       int64_t bsh, int n, PackedView outb, float range, hipStream_t stream,
+                                       uint32_t *zero_words = nullptr, int nzero = 0);
 // One launch, W read once: single-pass W strips (K <= 4096, n % 8 == 0: 8-column strips at two blocks
 // per CU, or 16-column strips) + X rows.  hipErrorNotSupported when the shape/layout is outside that
 // (caller falls back).
+// zero_words/nzero: words zeroed by block 0 of the launch (the GEMM's split-K tickets)
 hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream);
+                                   int64_t wsh, int n, PackedView outw, float range, hipStream_t stream,
+                                   uint32_t *zero_words = nullptr, int nzero = 0);
 // kind 8 / 16 forces the strip width (lab); 0 chooses.
 hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                        int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind);
+                                        int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind,
+                                        uint32_t *zero_words = nullptr, int nzero = 0);
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
@@ -113,6 +117,8 @@ size_t gemm_scratch_bytes(int m, int n, int k);
 // bias (n floats) != nullptr: y = fl(O + b[j]) (+ relu): the encoder's linear layers.
 // tickets_zeroed: the split-K scratch is library-owned, zeroed once at allocation; the launch's
 // reducers re-zero their tickets instead of a memset ahead of every launch.
+// bytes at the start of the split-K scratch that must be zero before a split launch (0: no split)
+size_t gemm_ticket_bytes(int m, int n, int k);
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
                                int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
                                const float *bias = nullptr, bool relu = false, bool tickets_zeroed = false);

@@ -115,6 +115,33 @@ def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
     assert_bits_equal(_run_full(qg, X, W, device), want, f"{M}x{N}x{K} op_quantized_mm")
 
 
+@pytest.mark.parametrize("M,N,K,layout", [(256, 256, 4096, "rows"), (300, 520, 4500, "rows"), (256, 512, 2048, "rows"),
+                                          (256, 256, 4096, "generic")])
+def test_split_k_poisoned_caller_workspace(qg, oracle, device, M, N, K, layout):
+    """op_mm_quantize_ws on a workspace full of 0xFF at split-K shapes: the split-K tickets at its start
+    are zeroed by the pack launch (single pass, or the row/column-absmax launch for K > 4096) or by the
+    GEMM's own zeroing launch (generic strides: separate pack launches)."""
+    X, W = oracle.inputs(M, N, K, 91)
+    want = oracle.quantized_mm(X, W)
+    L = qg.load()
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    if layout == "generic":  # every other column of a wider buffer: the strided (fallback) pack path
+        Xd = _dev(np.repeat(X, 2, axis=1), device)[:, ::2]
+    a256 = lambda b: (b + 255) // 256 * 256  # noqa: E731
+    assert L.op_mm_quantize_workspace_size(M, N, K) > a256(L.qgemm_packed_size(M, K)) + a256(L.qgemm_packed_size(N, K)), \
+        "shape expected to run split-K"
+    ws = torch.full((L.op_mm_quantize_workspace_size(M, N, K),), 255, dtype=torch.uint8, device=device)
+    s = qg._stream(device)
+    for i in range(2):
+        O = torch.full((M, N), float("nan"), device=device)
+        rc = L.op_mm_quantize_ws(Xd.data_ptr(), Xd.stride(0), Xd.stride(1), Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M,
+                                 N, K, 127.0, ws.data_ptr(), ws.numel(), s)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} {layout} call {i}")
+        ws.fill_(255)
+
+
 def test_split_k_shapes_share_library_scratch(qg, oracle, device):
     """Different split-K plans one after another on the same stream share qgemm_mm_packed's scratch
     (tickets zeroed once, re-zeroed by each launch's reducers): every call stays bit-exact."""
