@@ -47,6 +47,11 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+// wave-uniform buffer descriptor over [base, base + bytes): loads past the end return zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
+}
+
 // The GEMM's split-K tickets live in the caller's workspace, whose contents are arbitrary: the pack
 // launch that precedes the GEMM in the same stream zeroes them (block 0), which saves the GEMM a
 // zeroing launch of its own.
@@ -64,7 +69,7 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = blk * 4 + (threadIdx.x >> 6);
+    const int64_t row = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     if (row >= rows_pad) return;
     uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
     const int64_t nq = k_pad >> 2;  // uint32 words per packed row
@@ -81,10 +86,13 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     float p = -INFINITY;
     float4 v[R > 0 ? R : 1];
     if constexpr (R > 0) {
+        // buffer loads on one per-lane offset; chunks >= nfull lie past the descriptor and read as zeros
+        typedef int v4i_t __attribute__((ext_vector_type(4)));
+        const auto rs = buf_rsrc(srow, (uint32_t)nfull * 16);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const int c = lane + j * kWave;
-            v[j] = (c < nfull) ? s4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, 0);
+            v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -554,10 +562,6 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
 // n = 8192 at K >= 2048, worse for wider W (n = 12288, 16384) and short K, where the 16-column pass stays.
 constexpr int kWs8Cols = 8;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
-}
-
 __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                    float range, float *__restrict__ scale, int8_t *__restrict__ q,
                                                    int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */) {
@@ -637,7 +641,8 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     }
 }
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 5))) void pack_single_pass8_kernel(
+template <int kWavesPerEu>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu, kWavesPerEu))) void pack_single_pass8_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
     int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero) {
@@ -755,7 +760,7 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
         const int nstrips = n / kWs8Cols;
         const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
         const int nx = (int)(outx.rows_pad / 8);
-        pack_single_pass8_kernel<<<nstrips + npad + nx, 512, 0, stream>>>(x, xsh, m, k, outx.scale, outx.q,
+        pack_single_pass8_kernel<5><<<nstrips + npad + nx, 512, 0, stream>>>(x, xsh, m, k, outx.scale, outx.q,
                                                                           outx.rows_pad, outx.k_pad, w, wsh, n,
                                                                           outw.scale, outw.q, outw.rows_pad, nstrips,
                                                                           range, zero_words, nzero);

@@ -2,7 +2,8 @@
 // W strips (1024-thread blocks, one per CU) against 8-column strips (512-thread blocks, two per CU),
 // bit-compared.  Experiments measured here and dropped: 1024-thread 8-column blocks forced to 64
 // VGPRs (two blocks per CU, X rows two waves each): spills, 36.7 us at 4096^3; a dispatch order that
-// sweeps the columns chip-wide instead of XCD-contiguous strip ranges: +13 us at n = 16384.
+// sweeps the columns chip-wide instead of XCD-contiguous strip ranges: +13 us at n = 16384; the
+// 8-column kernel held to 80 VGPRs for three blocks per CU: 8 VGPRs spilled, 33.4 vs 28.8 us.
 // Build: make -C .. pack2lab   Run: build/pack2_lab [m n k reps]
 #include <cstdio>
 #include <cstdlib>
