@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-error-stats", action="store_true", help="skip the post-run quantization-error check")
+    p.add_argument("--cold-steps", type=int, default=20,
+                   help="after the timed region: calls timed one by one after a 1-GiB read sweep that evicts the "
+                        "inputs from the 256-MB Infinity Cache (0 = skip); reported beside the warm steady state")
     p.add_argument("--gather", action="store_true", help="also time the whole-node all-gather of C (N>1)")
     p.add_argument("--gemm-timing-every", type=int, default=5,
                    help="time the GEMM kernel on every n-th timed step (events cost ~4 us per timed step)")
@@ -279,6 +282,28 @@ def main():
     }
     if gather_ms is not None:
         result["allgather_C_ms"] = round(gather_ms, 3)
+    if rank == 0 and args.cold_steps > 0:
+        # Steady-state steps re-read the same X and W, which (with O) fit in the 256-MB Infinity Cache;
+        # this is the same call with them evicted first (a 1-GiB read sweep between calls), each call timed
+        # alone by events on its stream (includes the launch of its first kernel)
+        flush = torch.ones(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB, read (not written) per sweep
+        ev = HipEvents(2)
+        cold = []
+        for i in range(args.cold_steps):
+            flush.sum()  # clean lines: no write-back of the sweep competes with the call
+            torch.cuda.synchronize(dev)
+            ev.hip.hipEventRecord(ev.ev[0], s)
+            step()
+            ev.hip.hipEventRecord(ev.ev[1], s)
+            cold.append(ev.elapsed_ms(ev.ev[0], ev.ev[1]))
+        ev.destroy()
+        del flush
+        cold.sort()
+        result["cold_cache"] = {
+            "ms_per_call_median": round(cold[len(cold) // 2], 5), "ms_per_call_min": round(cold[0], 5),
+            "calls": len(cold),
+            "note": "each call after a 1-GiB read sweep evicted X, W and O from the Infinity Cache; value above is the "
+                    "warm steady state (same inputs every step, as GEMM benchmarks run)"}
     if rank == 0 and not args.no_error_stats:
         # after the timed region: the quantization error of this run's output against the reference's
         # unquantized op_mm (qgemm_mm_fp32, bit-exact sequential-k fmaf), computed on the device

@@ -65,6 +65,24 @@ int main(int argc, char **argv) {
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             t[i].push_back(ms * 1000 / reps);
         }
+    // cold-cache timing: a 1-GiB sweep (memset) between launches evicts the inputs from the 256-MB
+    // Infinity Cache; each launch is timed alone with events
+    {
+        void *flush; const size_t fb = (size_t)1 << 30;
+        CK(hipMalloc(&flush, fb));
+        hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
+        for (size_t i = 0; i < vs.size(); ++i) {
+            std::vector<float> v;
+            for (int r = 0; r < 15; ++r) {
+                CK(hipMemsetAsync(flush, r, fb, s0));
+                CK(hipEventRecord(a, s0)); vs[i].f(); CK(hipEventRecord(z, s0)); CK(hipEventSynchronize(z));
+                float ms; CK(hipEventElapsedTime(&ms, a, z)); v.push_back(ms * 1000);
+            }
+            std::sort(v.begin(), v.end());
+            printf("%-14s cold median %8.2f us  min %8.2f us\n", vs[i].name, v[v.size() / 2], v[0]);
+        }
+        CK(hipFree(flush));
+    }
     const double bytes = 4.0 * m * k + 4.0 * k * n + (double)m * k + (double)k * n;
     for (size_t i = 0; i < vs.size(); ++i) {
         auto v = t[i]; std::sort(v.begin(), v.end());
