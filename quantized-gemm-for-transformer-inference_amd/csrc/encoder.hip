@@ -79,12 +79,15 @@ hipError_t make_packed(int k, int n, const std::vector<uint64_t> &col_seeds, int
     return launch_pack_cols(tmp, n, k, n, 127.0f, packed_view(*packed, n, k), s);
 }
 
+// the packed activations of the next linear (one buffer, reused by every linear in stream order)
+PackedView act_view(Encoder &E, int seq, int k) { return packed_view(E.ws + E.scratch_bytes, seq, k); }
+
+// x == nullptr: the activations are already packed in act_view (by the add+layernorm that made them)
 hipError_t linear(Encoder &E, const float *x, int seq, int k, const void *wpacked, int n, float *y,
                   const float *bias, bool relu, hipStream_t s) {
     // pack the activations (Cx per row: op_absmax(X), X_int8), then the GEMM with the fused epilogue
-    char *pa = E.ws + E.scratch_bytes;
-    const PackedView va = packed_view(pa, seq, k);
-    hipError_t e = launch_pack_rows(x, k, 1, seq, k, 127.0f, va, s);
+    const PackedView va = act_view(E, seq, k);
+    hipError_t e = x ? launch_pack_rows(x, k, 1, seq, k, 127.0f, va, s) : hipSuccess;
     if (e != hipSuccess) return e;
     const float inv_r2 = 1.0f / (127.0f * 127.0f);
     return launch_gemm_dequant(va, packed_view(wpacked, n, k), y, n, 1, seq, n, inv_r2, E.ws, E.scratch_bytes, s,
@@ -182,12 +185,14 @@ hipError_t encoder_forward(Encoder *E, const float *X, float *Y, int seq, hipStr
     const int d = E->d_model, H = E->n_heads, dk = d / H;
     const float scale = (float)(1.0 / std::sqrt((double)dk));  // attention.cuh:64
     const float *in = X;
+    bool in_packed = false;  // the previous block's last add+layernorm packed its output already
     hipError_t e;
     for (int i = 0; i < E->n_blocks; ++i) {
         const EncoderBlock &B = E->blocks[i];
-        float *out = (i == E->n_blocks - 1) ? Y : (i % 2 ? E->xb : E->xa);
+        const bool last = i == E->n_blocks - 1;
+        float *out = last ? Y : (i % 2 ? E->xb : E->xa);
         // [Q | K | V] = X @ [Wq | Wk | Wv]                              (attention.cuh:54-56, all heads)
-        if ((e = linear(*E, in, seq, d, B.wqkv, 3 * d, E->qkv, nullptr, false, s))) return e;
+        if ((e = linear(*E, in_packed ? nullptr : in, seq, d, B.wqkv, 3 * d, E->qkv, nullptr, false, s))) return e;
         // S_h = Q_h K_h^T, fp32 op_mm with the transposed view           (attention.cuh:58-60)
         if ((e = launch_mm_f32_batched(E->qkv, 3 * d, 1, dk, E->qkv + d, 1, 3 * d, dk, E->scores, seq, 1,
                                        (int64_t)seq * seq, seq, seq, dk, H, s)))
@@ -200,12 +205,17 @@ hipError_t encoder_forward(Encoder *E, const float *X, float *Y, int seq, hipStr
             return e;
         // output = multiHeadOut @ W_O; LN(output + multiHeadOut)         (transformer.cu:52-59)
         if ((e = linear(*E, E->heads, seq, d, B.wo, d, E->t, nullptr, false, s))) return e;
-        if ((e = launch_add_layernorm_rows(E->t, E->heads, E->x1, seq, d, s))) return e;
+        // (x1 is packed by the same launch: the FFN's first linear quantizes nothing itself)
+        if ((e = launch_add_layernorm_rows_pack(E->t, E->heads, E->x1, seq, d, 127.0f, act_view(*E, seq, d), s)))
+            return e;
         // FFN: relu(x1 W1 + b1) W2 + b2; LN(ffn + multiHeadOut)          (transformer.cu:62-75)
-        if ((e = linear(*E, E->x1, seq, d, B.w1, E->d_ff, E->ffn, B.b1, true, s))) return e;
+        if ((e = linear(*E, nullptr, seq, d, B.w1, E->d_ff, E->ffn, B.b1, true, s))) return e;
         if ((e = linear(*E, E->ffn, seq, E->d_ff, B.w2, d, E->t, B.b2, false, s))) return e;
-        if ((e = launch_add_layernorm_rows(E->t, E->heads, out, seq, d, s))) return e;
+        e = last ? launch_add_layernorm_rows(E->t, E->heads, out, seq, d, s)
+                 : launch_add_layernorm_rows_pack(E->t, E->heads, out, seq, d, 127.0f, act_view(*E, seq, d), s);
+        if (e) return e;
         in = out;
+        in_packed = !last;
     }
     return hipSuccess;
 }

@@ -72,13 +72,28 @@ __global__ __launch_bounds__(64 * kRowWaves) void softmax_rows_kernel(const floa
     for (int c = lane; c < w; c += 64) p[c] = __fdiv_rn(st[c], sum);
 }
 
+// kPack: also quantize the output row for the next quantized linear (the pack_rows step of
+// linear(), fused): absmax with the signed seed y[0] over |y[c]|, c >= 1 (maxnum: NaN never wins),
+// s = fl(range / Cx), q = sat_i8(trunc(fl(y * s))) -- the same operations as pack_rows_vec_body, so
+// the packed row is bit-identical to packing Y afterwards.  Rows [rows, rows_pad) of the packed view
+// get zero bytes and a zero scale; columns [w, k_pad) zero bytes.
+template <bool kPack>
 __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(const float *__restrict__ A,
                                                                             const float *__restrict__ B,
                                                                             float *__restrict__ Y, int64_t rows,
-                                                                            int w) {
+                                                                            int w, int8_t *__restrict__ q,
+                                                                            float *__restrict__ qscale,
+                                                                            int64_t k_pad, int64_t rows_pad,
+                                                                            float range) {
     extern __shared__ __attribute__((aligned(16))) float stage[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
+    if (kPack && row >= rows && row < rows_pad) {  // padding row of the packed view
+        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+        for (int64_t c = lane; c < k_pad / 4; c += 64) qrow[c] = 0u;
+        if (lane == 0) qscale[row] = 0.0f;
+        return;
+    }
     if (row >= rows) return;
     const float *a = A + row * w, *b = B + row * w;
     float *y = Y + row * w;
@@ -97,8 +112,33 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     const float var = __fdiv_rn(seq_sum(st, w), fw);           // :21-25
-    for (int c = lane; c < w; c += 64)                         // (x - mean) / var (:28), as written
-        y[c] = __fdiv_rn(__fsub_rn(__fadd_rn(a[c], b[c]), mean), var);
+    float cand = -INFINITY;
+    __builtin_amdgcn_wave_barrier();
+    for (int c = lane; c < w; c += 64) {                       // (x - mean) / var (:28), as written
+        const float v = __fdiv_rn(__fsub_rn(__fadd_rn(a[c], b[c]), mean), var);
+        y[c] = v;
+        if constexpr (kPack) {
+            st[c] = v;  // each lane overwrites only the columns it owns
+            if (c > 0) cand = fmaxf(cand, absmax_candidate(v));
+        }
+    }
+    if constexpr (kPack) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) cand = fmaxf(cand, __shfl_xor(cand, off, 64));
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const float cx = absmax_finish(st[0], cand);
+        const float sc = inv_divide(range, cx);
+        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+        for (int c4 = lane; c4 < (int)(k_pad / 4); c4 += 64) {
+            int qb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) qb[e] = 4 * c4 + e < w ? quant_i8(st[4 * c4 + e], sc) : 0;
+            qrow[c4] = (uint32_t)(qb[0] & 0xff) | ((uint32_t)(qb[1] & 0xff) << 8) | ((uint32_t)(qb[2] & 0xff) << 16) |
+                       ((uint32_t)(qb[3] & 0xff) << 24);
+        }
+        if (lane == 0) qscale[row] = cx;
+    }
 }
 
 }  // namespace
@@ -117,8 +157,17 @@ hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, i
     if (w < 1 || w > kMaxRowLen || rows < 0) return hipErrorInvalidValue;
     if (rows == 0) return hipSuccess;
     const size_t lds = sizeof(float) * kRowWaves * ((w + 3) & ~3);
-    add_layernorm_rows_kernel<<<(unsigned)((rows + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds, stream>>>(
-        A, B, Y, rows, w);
+    add_layernorm_rows_kernel<false><<<(unsigned)((rows + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds, stream>>>(
+        A, B, Y, rows, w, nullptr, nullptr, 0, 0, 0.0f);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_layernorm_rows_pack(const float *A, const float *B, float *Y, int64_t rows, int w, float range,
+                                          PackedView out, hipStream_t stream) {
+    if (w < 1 || w > kMaxRowLen || rows < 1 || out.k_pad < w || out.rows_pad < rows) return hipErrorInvalidValue;
+    const size_t lds = sizeof(float) * kRowWaves * ((w + 3) & ~3);
+    add_layernorm_rows_kernel<true><<<(unsigned)((out.rows_pad + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds,
+                                      stream>>>(A, B, Y, rows, w, out.q, out.scale, out.k_pad, out.rows_pad, range);
     return hipGetLastError();
 }
 

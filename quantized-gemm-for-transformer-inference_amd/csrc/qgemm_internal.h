@@ -135,6 +135,9 @@ hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64
 hipError_t launch_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, hipStream_t stream);
 hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w,
                                      hipStream_t stream);
+// the same, also writing Y's rows packed (Cx + int8) for the next quantized linear (pack_rows fused)
+hipError_t launch_add_layernorm_rows_pack(const float *A, const float *B, float *Y, int64_t rows, int w, float range,
+                                          PackedView out, hipStream_t stream);
 // LLM.int8() outlier decomposition (outlier.hip).
 size_t outlier_scratch_bytes(int m, int n, int k);
 hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, float t,
