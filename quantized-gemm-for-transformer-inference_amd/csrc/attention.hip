@@ -1,0 +1,238 @@
+// attention.hip -- the encoder's fp32 attention core (attention.cuh:58-69) in ONE launch per block of
+// the encoder: for every (head, 32-query tile) a workgroup computes
+//   S = Q_h K_h^T                  op_mm<float> on the transposed view    (attention.cuh:58-60)
+//   P = softmax(S * 1/sqrt(d_k))   op_multiply + op_softmax               (attention.cuh:65-68)
+//   heads[:, h*d_k..] = P V_h      op_mm<float>                           (attention.cuh:69)
+// with S and P kept in LDS (the three-launch form writes and re-reads the H x seq x seq score tensor
+// through HBM twice).  Every step keeps the arithmetic of the separate kernels bit for bit:
+//   * both products are v_mfma_f32_16x16x4_f32 chains from +0 over k ascending, zero-padded to a
+//     multiple of 4, then fl(res + 0) when k % 32 != 0 -- the reference's op_matmul_kernel chain
+//     (op_mm.cuh:37-39) with its zero-padded last 32-wide tile, exactly as gemm_f32.hip;
+//   * softmax as softmax_rows_kernel: products fl(s * scale), max seeded by the first element with a
+//     strict >, correctly rounded fp32 exp of fl(x - max), ONE sequential fp32 sum in column order,
+//     then fl(e / sum).
+// Envelope: d_k <= 64, seq <= 512 (S tile 32 x 512 fp32 = 64 KiB of LDS, Q tile and K / V staged
+// through LDS in 256-key chunks: 155 KiB in all); outside it the encoder runs the three kernels.
+#include "qgemm_internal.h"
+
+namespace qgemm {
+
+namespace {
+
+constexpr int kTQ = 32;                    // query rows per workgroup
+constexpr int kAttnMaxSeq = 512;
+constexpr int kAttnMaxDk = 64;
+constexpr int kAttnThreads = 1024;         // 16 waves: 4 per SIMD hide the LDS and exp latencies
+constexpr int kSStride = kAttnMaxSeq + 4;  // S row stride (floats): consecutive rows 4 banks apart
+constexpr int kChunk = 256;                // keys per K / V chunk staged in LDS
+constexpr int kKStride = 68;               // K chunk [key][d_k]: B-fragment reads (16 keys x 4 k) conflict-free
+constexpr int kVStride = 80;               // V chunk [key][d_k]: B-fragment reads (4 keys x 16 cols) conflict-free
+constexpr int kKVFloats = kChunk * kVStride;
+constexpr int kQStride = 68;               // Q tile [query][d_k]: A-fragment reads conflict-free
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// kSkip (lab ablation only; 0 in the library): 1 = no QK^T MFMAs, 2 = no softmax, 4 = no PV MFMAs,
+// 8 = no sequential sums, 16 = s_memrealtime stamps at the phase boundaries (g_attn_stamp)
+__device__ unsigned long long g_attn_stamp[4096][6];
+template <int kSkip = 0>
+__global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const float *__restrict__ qkv, int d, int dk,
+                                                                       int seq, float scale, float *__restrict__ heads) {
+    __shared__ __attribute__((aligned(16))) float S[kTQ * kSStride];
+    __shared__ __attribute__((aligned(16))) float KV[kKVFloats];
+    __shared__ __attribute__((aligned(16))) float Qs[kTQ * kQStride];
+    const int h = blockIdx.y, q0 = blockIdx.x * kTQ;
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t ld = 3 * (int64_t)d;
+    const float *Qb = qkv + (int64_t)h * dk, *Kb = qkv + d + (int64_t)h * dk, *Vb = qkv + 2 * (int64_t)d + (int64_t)h * dk;
+    const int lr = lane & 15, lk = lane >> 4;  // MFMA operand lane: row lr of the fragment, k offset lk
+    const int rows = seq - q0 < kTQ ? seq - q0 : kTQ;
+    const int nchunks = (seq + kChunk - 1) / kChunk;
+    const int dk4 = (dk + 3) >> 2;  // float4 columns of a K / V row (the last one zero-padded)
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr ((kSkip & 16) != 0)
+            if (t == 0) g_attn_stamp[bid & 4095][i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
+
+    // stage keys [c0, c0 + 256) of K or V into KV ([key][stride], zero past seq and past d_k)
+    auto stage = [&](const float *src, int c0, int stride) __attribute__((always_inline)) {
+        for (int f = t; f < kChunk * 16; f += kAttnThreads) {
+            const int row = f >> 4, c4 = f & 15, j = c0 + row;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < seq && c4 < dk4) {
+                const float *p = src + j * ld + 4 * c4;
+                if (4 * c4 + 3 < dk && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+                    v = *reinterpret_cast<const float4 *>(p);
+                } else {
+                    v.x = p[0];
+                    v.y = 4 * c4 + 1 < dk ? p[1] : 0.f;
+                    v.z = 4 * c4 + 2 < dk ? p[2] : 0.f;
+                    v.w = 4 * c4 + 3 < dk ? p[3] : 0.f;
+                }
+            }
+            *reinterpret_cast<float4 *>(KV + row * stride + 4 * c4) = v;
+        }
+    };
+
+    // ---- S[32][seq] = Q K^T, one K chunk at a time: wave w computes 16-column tile w of the chunk for
+    // both 16-row halves (one B fragment, two A fragments)
+    const int ns = dk4;  // k-steps (<= 16)
+    // the Q tile through LDS (coalesced row loads once per workgroup, not per wave), with K chunk 0
+    for (int f = t; f < kTQ * 16; f += kAttnThreads) {
+        const int row = f >> 4, c4 = f & 15, i = q0 + row;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < seq && c4 < dk4) {
+            const float *p = Qb + i * ld + 4 * c4;
+            v.x = p[0];
+            v.y = 4 * c4 + 1 < dk ? p[1] : 0.f;
+            v.z = 4 * c4 + 2 < dk ? p[2] : 0.f;
+            v.w = 4 * c4 + 3 < dk ? p[3] : 0.f;
+        }
+        *reinterpret_cast<float4 *>(Qs + row * kQStride + 4 * c4) = v;
+    }
+    float qa[2][16];
+    const bool padk = (dk % 32) != 0;
+    for (int c = 0; c < nchunks; ++c) {
+        if (c) __syncthreads();  // every wave is done with the previous chunk
+        stage(Kb, c * kChunk, kKStride);
+        __syncthreads();
+        if (c == 0) {
+#pragma unroll
+            for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+                for (int s = 0; s < 16; ++s) qa[rf][s] = Qs[(rf * 16 + lr) * kQStride + 4 * s + lk];
+            stamp(1);
+        }
+        const int col = c * kChunk + wave * 16 + lr;
+        if (c * kChunk + wave * 16 < seq) {
+            const float *krow = KV + (wave * 16 + lr) * kKStride + lk;
+            v4f a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                if (s < ns && !(kSkip & 1)) {  // wave-uniform: no zero k-steps past the padded d_k (-0 would become +0)
+                    const float kb = krow[4 * s];
+                    a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[0][s], kb, a0, 0, 0, 0);
+                    a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[1][s], kb, a1, 0, 0, 0);
+                }
+            if (col < seq) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    S[(4 * lk + r) * kSStride + col] = padk ? __fadd_rn(a0[r], 0.0f) : a0[r];
+                    S[(16 + 4 * lk + r) * kSStride + col] = padk ? __fadd_rn(a1[r], 0.0f) : a1[r];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    stamp(2);
+
+    // ---- softmax of rows 2w and 2w+1: max and exp across the lanes; the two sequential sums at once
+    // (lanes 0 and 1); the division across the lanes
+    for (int rr = 0; rr < 2 && !(kSkip & 2); ++rr) {
+        const int rl = wave * 2 + rr;
+        if (rl >= rows) break;
+        float *srow = S + rl * kSStride;
+        const float seed = __fmul_rn(srow[0], scale);
+        float cand = -INFINITY;
+        for (int c = lane + 1; c < seq; c += 64) {
+            const float x = __fmul_rn(srow[c], scale);  // op_multiply(QK_T, scale_factor)
+            cand = (x > cand) ? x : cand;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float o = __shfl_xor(cand, off, 64);
+            cand = (o > cand) ? o : cand;
+        }
+        const float mx = (cand > seed) ? cand : seed;
+        for (int c = lane; c < seq; c += 64) srow[c] = (float)exp((double)__fsub_rn(__fmul_rn(srow[c], scale), mx));
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's exps are in LDS
+    __builtin_amdgcn_wave_barrier();
+    float sum = 0.0f;
+    if (lane < 2 && wave * 2 + lane < rows && !(kSkip & 8)) {
+        const float *srow = S + (wave * 2 + lane) * kSStride;
+        int c = 0;
+        for (; c + 4 <= seq; c += 4) {
+            const float4 v = *reinterpret_cast<const float4 *>(srow + c);
+            sum = __fadd_rn(sum, v.x);
+            sum = __fadd_rn(sum, v.y);
+            sum = __fadd_rn(sum, v.z);
+            sum = __fadd_rn(sum, v.w);
+        }
+        for (; c < seq; ++c) sum = __fadd_rn(sum, srow[c]);
+    }
+    for (int rr = 0; rr < 2 && !(kSkip & 2); ++rr) {
+        const int rl = wave * 2 + rr;
+        const float srr = __shfl(sum, rr, 64);
+        if (rl >= rows) break;
+        float *srow = S + rl * kSStride;
+        for (int c = lane; c < seq; c += 64) srow[c] = __fdiv_rn(srow[c], srr);
+    }
+
+    // ---- heads = P V, one V chunk at a time: waves 0 .. 2*ceil(d_k/16)-1 own output tile (row half
+    // w & 1, column tile w >> 1) and carry its accumulator across the chunks (the k chain stays in order)
+    const int nct2 = (dk + 15) >> 4, nks = (seq + 3) >> 2;
+    const bool padj = (seq % 32) != 0;
+    const bool pv_wave = wave < 2 * nct2;
+    const int rf = wave & 1, ct = wave >> 1;
+    const int col = ct * 16 + lr;
+    const float *prow = S + (rf * 16 + lr) * kSStride + lk;
+    v4f acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nchunks; ++c) {
+        __syncthreads();  // P complete (c = 0) / the previous V chunk consumed
+        if (c == 0) stamp(3);
+        stage(Vb, c * kChunk, kVStride);
+        __syncthreads();
+        if (c == 0) stamp(4);
+        if (pv_wave && !(kSkip & 4)) {
+            // the chunk's k-steps in groups of 16: group g+1's operands are read from LDS while group g's
+            // MFMAs run (the accumulation chain itself stays in k order)
+            const int s_beg = c * (kChunk / 4), s_end = min(nks, (c + 1) * (kChunk / 4));
+            const float *vcol = KV + lk * kVStride + col;
+            auto read = [&](float (&pa)[16], float (&vb)[16], int s0) __attribute__((always_inline)) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int s = s0 + u, j = 4 * s + lk;
+                    pa[u] = j < seq ? prow[4 * s] : 0.0f;  // S past seq is not written
+                    vb[u] = s < s_end ? vcol[(4 * s - c * kChunk) * kVStride] : 0.0f;
+                }
+            };
+            float pa0[16], vb0[16], pa1[16], vb1[16];
+            if (s_beg < s_end) read(pa0, vb0, s_beg);
+            for (int s0 = s_beg; s0 < s_end; s0 += 32) {
+                if (s0 + 16 < s_end) read(pa1, vb1, s0 + 16);
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (s0 + u < s_end) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[u], vb0[u], acc, 0, 0, 0);
+                if (s0 + 32 < s_end) read(pa0, vb0, s0 + 32);
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (s0 + 16 + u < s_end) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[u], vb1[u], acc, 0, 0, 0);
+            }
+        }
+    }
+    stamp(5);
+    if (pv_wave && col < dk) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rl = rf * 16 + 4 * lk + r;
+            if (rl < rows) heads[(int64_t)(q0 + rl) * d + (int64_t)h * dk + col] = padj ? __fadd_rn(acc[r], 0.0f) : acc[r];
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_attention_fused(const float *qkv, int seq, int d, int n_heads, float scale, float *heads,
+                                  hipStream_t stream) {
+    if (n_heads < 1 || d % n_heads) return hipErrorInvalidValue;
+    const int dk = d / n_heads;
+    if (seq < 1 || seq > kAttnMaxSeq || dk > kAttnMaxDk) return hipErrorNotSupported;
+    attention_fused_kernel<0><<<dim3((unsigned)((seq + kTQ - 1) / kTQ), (unsigned)n_heads), kAttnThreads, 0, stream>>>(
+        qkv, d, dk, seq, scale, heads);
+    return hipGetLastError();
+}
+
+}  // namespace qgemm

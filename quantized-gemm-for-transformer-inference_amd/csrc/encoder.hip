@@ -193,16 +193,19 @@ hipError_t encoder_forward(Encoder *E, const float *X, float *Y, int seq, hipStr
         float *out = last ? Y : (i % 2 ? E->xb : E->xa);
         // [Q | K | V] = X @ [Wq | Wk | Wv]                              (attention.cuh:54-56, all heads)
         if ((e = linear(*E, in_packed ? nullptr : in, seq, d, B.wqkv, 3 * d, E->qkv, nullptr, false, s))) return e;
-        // S_h = Q_h K_h^T, fp32 op_mm with the transposed view           (attention.cuh:58-60)
-        if ((e = launch_mm_f32_batched(E->qkv, 3 * d, 1, dk, E->qkv + d, 1, 3 * d, dk, E->scores, seq, 1,
-                                       (int64_t)seq * seq, seq, seq, dk, H, s)))
-            return e;
-        // P_h = softmax(S_h * 1/sqrt(d_k)), in place                     (attention.cuh:65-68)
-        if ((e = launch_softmax_rows(E->scores, E->scores, (int64_t)H * seq, seq, scale, s))) return e;
-        // heads[:, h*d_v..] = P_h V_h                                    (attention.cuh:69, transformer.cu:43-50)
-        if ((e = launch_mm_f32_batched(E->scores, seq, 1, (int64_t)seq * seq, E->qkv + 2 * d, 3 * d, 1, dk, E->heads,
-                                       d, 1, dk, seq, dk, seq, H, s)))
-            return e;
+        // S_h = Q_h K_h^T, P_h = softmax(S_h * 1/sqrt(d_k)), heads[:, h*d_v..] = P_h V_h
+        // (attention.cuh:58-69, transformer.cu:43-50): one launch with S in LDS where it fits
+        e = launch_attention_fused(E->qkv, seq, d, H, scale, E->heads, s);
+        if (e == hipErrorNotSupported) {
+            // fp32 op_mm with the transposed view, softmax in place, fp32 op_mm into the head's columns
+            if ((e = launch_mm_f32_batched(E->qkv, 3 * d, 1, dk, E->qkv + d, 1, 3 * d, dk, E->scores, seq, 1,
+                                           (int64_t)seq * seq, seq, seq, dk, H, s)))
+                return e;
+            if ((e = launch_softmax_rows(E->scores, E->scores, (int64_t)H * seq, seq, scale, s))) return e;
+            e = launch_mm_f32_batched(E->scores, seq, 1, (int64_t)seq * seq, E->qkv + 2 * d, 3 * d, 1, dk, E->heads, d, 1,
+                                      dk, seq, dk, seq, H, s);
+        }
+        if (e) return e;
         // output = multiHeadOut @ W_O; LN(output + multiHeadOut)         (transformer.cu:52-59)
         if ((e = linear(*E, E->heads, seq, d, B.wo, d, E->t, nullptr, false, s))) return e;
         // (x1 is packed by the same launch: the FFN's first linear quantizes nothing itself)

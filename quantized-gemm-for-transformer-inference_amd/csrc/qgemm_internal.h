@@ -132,6 +132,11 @@ hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64
                                  int n, int k, int batch, hipStream_t stream);
 // Encoder row ops (encoder_ops.hip): the reference's op_softmax (after op_multiply by `scale`) and
 // op_add + op_layernorm, one row per wave, sums in the reference's sequential order.
+// S = QK^T, softmax(S * scale), heads = PV for every head in one launch (S in LDS), bit-identical to
+// the three separate kernels; hipErrorNotSupported outside d_k <= 64, seq <= 512 (caller falls back).
+// qkv: seq x 3d ([Q | K | V], head h at columns h*d_k of each third); heads: seq x d.
+hipError_t launch_attention_fused(const float *qkv, int seq, int d, int n_heads, float scale, float *heads,
+                                  hipStream_t stream);
 hipError_t launch_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, hipStream_t stream);
 hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, int64_t rows, int w,
                                      hipStream_t stream);
