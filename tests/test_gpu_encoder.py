@@ -53,6 +53,10 @@ def test_linear_fused_bias_relu_bit_exact(qg, oracle, device, M, N, K, bias, rel
     (6, 8, 4, 8, 2),          # the reference's own Encoder call (transformer.cu:171-178)
     (32, 64, 4, 128, 2),
     (100, 256, 8, 512, 3),    # ragged seq, odd block count
+    (257, 96, 3, 64, 1),      # fused attention: d_k 32 (no +0 step), a second 256-key chunk holding one key
+    (40, 60, 5, 32, 2),       # d_k 12: k % 4 == 0, k % 32 != 0
+    (300, 128, 1, 64, 1),     # d_k 128 > 64: the three-launch attention fallback
+    (600, 64, 2, 64, 1),      # seq 600 > 512: fallback
 ])
 def test_encoder_forward_bit_exact(qg, oracle, device, seq, d, H, dff, blocks):
     X = oracle.uniform((seq, d), 11)
