@@ -29,13 +29,16 @@ static bool shape_ok(const PackedView &a, const PackedView &b) {
     return a.k_pad == b.k_pad && a.rows_pad % BM == 0 && b.rows_pad % BN == 0 && a.k_pad % BK == 0;
 }
 
-// Launch plan.  256 x 256 tiles (gemm_i8_v3) while they give >= 128 blocks; below that the 128 x 128
-// kernel (gemm_i8_t128, two blocks per CU).  Then split-K when the tiles alone leave CUs idle:
-// S = min(256 / tiles, k-steps / 8, 8) slices per tile -- every slice keeps >= 8 k-steps (K >= 1024),
-// since the slab round trip costs ~3-5 us (scripts/split_probe.py: at M = 512, K = 1024 every split
-// was slower; K = 4096 split 4 was fastest; 2048^3 on 128-tiles unsplit beat split 2).
+// Launch plan.  256 x 256 tiles (gemm_i8_v3) while they give >= 128 blocks, with split-K below 160
+// tiles when K is long: S = min(256 / tiles, k-steps / 8, 8) -- every slice keeps >= 8 k-steps
+// (scripts/split_probe.py: the slab round trip costs ~3-5 us).  Fewer 256-tiles: 64 x 64 tiles
+// (gemm_i8_small<64>, four blocks per CU) with S = min(512 / tiles, k-steps / 16, 4) slices -- splits
+// only for K >= 4096.  Measured (gemm_lab small mode, us, 128-tiles vs 64-tiles at the chosen S):
+// 512x3072x1024 11.8 -> 7.6, 512x1024x1024 11.1 -> 6.1, 512x4096x1024 12.2 -> 8.1,
+// 512x1024x4096 16.8 (S4) -> 10.9 (S2), 256x4096x4096 20.2 (S2) -> 13.2 (S2), 2048^3 20.7 -> 18.5;
+// split-K never helped at K = 1024.
 struct GemmPlan {
-    int tile;       // 256 or 128
+    int tile;       // 256 or 64
     int tiles_m, tiles_n;
     int splits;
 };
@@ -43,18 +46,21 @@ struct GemmPlan {
 static GemmPlan gemm_plan(int m, int n, int k) {
     GemmPlan g{256, (int)(round_up(m, 256) / 256), (int)(round_up(n, 256) / 256), 1};
     if (m <= 0 || n <= 0 || k <= 0) return g;
-    const int target = 256;
-    int no_split = 160;
-    if ((int64_t)g.tiles_m * g.tiles_n < 128) {
-        g = GemmPlan{128, (int)(round_up(m, 128) / 128), (int)(round_up(n, 128) / 128), 1};
-        no_split = 256;
-    }
-    const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
     const int nk = (int)(round_up(k, BK) / BK);
-    if (tiles >= no_split) return g;
-    int sp = (int)(target / tiles);
-    sp = sp < nk / 8 ? sp : nk / 8;
-    sp = sp < 8 ? sp : 8;
+    int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
+    if (tiles >= 128) {
+        if (tiles >= 160) return g;
+        int sp = (int)(256 / tiles);
+        sp = sp < nk / 8 ? sp : nk / 8;
+        sp = sp < 8 ? sp : 8;
+        g.splits = sp > 1 ? sp : 1;
+        return g;
+    }
+    g = GemmPlan{64, (int)(round_up(m, 64) / 64), (int)(round_up(n, 64) / 64), 1};
+    tiles = (int64_t)g.tiles_m * g.tiles_n;
+    int sp = tiles >= 512 ? 1 : (int)(512 / tiles);
+    sp = sp < nk / 16 ? sp : nk / 16;
+    sp = sp < 4 ? sp : 4;
     g.splits = sp > 1 ? sp : 1;
     return g;
 }
@@ -101,15 +107,16 @@ static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     return e;
 }
 
-template <int kEpi>
-static hipError_t launch_t128(const GemmArgs &p, dim3 grid, hipStream_t stream) {
+template <int TB, int kEpi>
+static hipError_t launch_small(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     const GemmEvents ev = take_gemm_events();
     if ((ev.start || ev.stop) && g_event_mode == 0) {
-        hipExtLaunchKernelGGL((gemm_i8_t128<kEpi>), grid, dim3(t128::kThreads), 0, stream, ev.start, ev.stop, 0, p);
+        hipExtLaunchKernelGGL((gemm_i8_small<TB, kEpi>), grid, dim3(SmallTile<TB>::kThreads), 0, stream, ev.start,
+                              ev.stop, 0, p);
         return hipGetLastError();
     }
     if (ev.start) (void)hipEventRecord(ev.start, stream);
-    gemm_i8_t128<kEpi><<<grid, dim3(t128::kThreads), 0, stream>>>(p);
+    gemm_i8_small<TB, kEpi><<<grid, dim3(SmallTile<TB>::kThreads), 0, stream>>>(p);
     hipError_t e = hipGetLastError();
     if (ev.stop) (void)hipEventRecord(ev.stop, stream);
     return e;
@@ -137,9 +144,9 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
         }
     }
     const dim3 grid((unsigned)(tiles * p.splits));
-    if (g.tile == 128) {
-        if (!bias) return launch_t128<kEpiNone>(p, grid, stream);
-        return relu ? launch_t128<kEpiBiasRelu>(p, grid, stream) : launch_t128<kEpiBias>(p, grid, stream);
+    if (g.tile == 64) {
+        if (!bias) return launch_small<64, kEpiNone>(p, grid, stream);
+        return relu ? launch_small<64, kEpiBiasRelu>(p, grid, stream) : launch_small<64, kEpiBias>(p, grid, stream);
     }
     if (!bias) return launch_v3<kEpiNone>(p, grid, stream);
     return relu ? launch_v3<kEpiBiasRelu>(p, grid, stream) : launch_v3<kEpiBias>(p, grid, stream);

@@ -508,22 +508,35 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// gemm_i8_t128: the 128 x 128 macro-tile for problems with few 256 x 256 tiles (the encoder's M = 512
-// linears, decode-sized M): 4 waves as 2 x 2, each 64 x 64 = 4 x 4 tiles of v_mfma_i32_16x16x64_i8,
-// the same staging (LDS-DMA, source-swizzled 128-B rows, 2-deep ring of 32-KiB stages), schedule and
-// split-K combine as gemm_i8_v3; the epilogue writes the whole 128 x 128 fp32 tile through the
-// 64-KiB ring at once.  Two blocks per CU.
-namespace t128 {
-constexpr int TB = 128;                       // macro-tile rows = cols
-constexpr int kThreads = 256;
-constexpr int kTileBytes = TB * BK;           // 16 KiB per operand per stage
-constexpr int kStageBytes = 2 * kTileBytes;
-constexpr int kLdsBytes = 2 * kStageBytes;    // 64 KiB
+// gemm_i8_small<TB>: TB x TB macro-tiles (TB = 128 or 64) for problems with few 256 x 256 tiles (the
+// encoder's M = 512 linears, decode-sized M): 4 waves as 2 x 2, each (TB/2) x (TB/2) = MI x MI tiles
+// of v_mfma_i32_16x16x64_i8, the same staging (LDS-DMA, source-swizzled 128-B rows, 2-deep ring),
+// schedule and split-K combine as gemm_i8_v3; the epilogue writes the whole TB x TB fp32 tile through
+// the ring at once.  TB = 128: 64-KiB ring, two blocks per CU; TB = 64: 32-KiB ring, four blocks per
+// CU -- four times the tiles, so shapes whose 128-tiles leave most CUs idle spread over the chip.
+template <int TB>
+struct SmallTile {
+    static constexpr int kThreads = 256;
+    static constexpr int WT = TB / 2;                // wave tile rows = cols
+    static constexpr int MI = WT / 16;               // 16 x 16 MFMA tiles per wave dimension
+    static constexpr int kRowsPerWave = TB / 4;      // staged rows per wave per operand
+    static constexpr int kPieces = kRowsPerWave / 8; // 1-KiB LDS-DMA pieces per operand per wave
+    static constexpr int kTileBytes = TB * BK;
+    static constexpr int kStageBytes = 2 * kTileBytes;
+    static constexpr int kLdsBytes = 2 * kStageBytes;
+    static constexpr int kMinBlocks = TB == 128 ? 2 : 4;
+    static_assert(TB * TB * 4 <= kLdsBytes, "epilogue image fits the ring");
+};
+namespace t128 {  // the 128-tile constants (launch shape)
+constexpr int TB = 128;
+constexpr int kThreads = SmallTile<128>::kThreads;
 }  // namespace t128
 
-template <int kEpi = kEpiNone>
-__global__ __launch_bounds__(t128::kThreads, 2) void gemm_i8_t128(GemmArgs p) {
-    __shared__ __attribute__((aligned(16))) int8_t lds[t128::kLdsBytes + 2048];  // + Cx, Cw, bias (128 each) + flag
+template <int TB, int kEpi = kEpiNone>
+__global__ __launch_bounds__(SmallTile<TB>::kThreads, SmallTile<TB>::kMinBlocks) void gemm_i8_small(GemmArgs p) {
+    using T_ = SmallTile<TB>;
+    constexpr int MI = T_::MI, WT = T_::WT, RPW = T_::kRowsPerWave, NP = T_::kPieces;
+    __shared__ __attribute__((aligned(16))) int8_t lds[T_::kLdsBytes + 4 * TB * 4];  // + Cx, Cw, bias, flag
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -535,59 +548,59 @@ __global__ __launch_bounds__(t128::kThreads, 2) void gemm_i8_t128(GemmArgs p) {
     const int nk_all = (int)(p.k_pad / BK);
     const int kt0 = slice * nk_all / S;
     const int nk = (slice + 1) * nk_all / S - kt0;
-    // staging: wave w fills rows [32w, 32w+32) of both tiles, 8 rows (1 KiB) per LDS-DMA, chunk g of
-    // row r at slot g ^ ((r>>1)&7)
-    const int8_t *Ablk = p.A + (int64_t)tm * t128::TB * p.k_pad;
-    const int8_t *Bblk = p.B + (int64_t)tn * t128::TB * p.k_pad;
-    int64_t src_off[4];
+    // staging: wave w fills rows [RPW w, RPW w + RPW) of both tiles, 8 rows (1 KiB) per LDS-DMA, chunk g
+    // of row r at slot g ^ ((r>>1)&7)
+    const int8_t *Ablk = p.A + (int64_t)tm * TB * p.k_pad;
+    const int8_t *Bblk = p.B + (int64_t)tn * TB * p.k_pad;
+    int64_t src_off[NP];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = wave * 32 + i * 8 + (lane >> 3);
+    for (int i = 0; i < NP; ++i) {
+        const int row = wave * RPW + i * 8 + (lane >> 3);
         src_off[i] = (int64_t)row * p.k_pad + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
     }
     auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
-        int8_t *la = lds + buf * t128::kStageBytes;
-        int8_t *lb = la + t128::kTileBytes;
+        int8_t *la = lds + buf * T_::kStageBytes;
+        int8_t *lb = la + T_::kTileBytes;
         const int8_t *ga = Ablk + (int64_t)kt * BK;
         const int8_t *gb = Bblk + (int64_t)kt * BK;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_global_load_lds((const void *)(ga + src_off[i]), (void *)(la + (wave * 32 + i * 8) * BK), 16,
+        for (int i = 0; i < NP; ++i) {
+            __builtin_amdgcn_global_load_lds((const void *)(ga + src_off[i]), (void *)(la + (wave * RPW + i * 8) * BK), 16,
                                              0, 0);
-            __builtin_amdgcn_global_load_lds((const void *)(gb + src_off[i]), (void *)(lb + (wave * 32 + i * 8) * BK), 16,
+            __builtin_amdgcn_global_load_lds((const void *)(gb + src_off[i]), (void *)(lb + (wave * RPW + i * 8) * BK), 16,
                                              0, 0);
         }
     };
     const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
-    const int a_row0 = (wm * 64 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    const int a_row0 = (wm * WT + lrow) * BK, b_row0 = (wn * WT + lrow) * BK;
     int off[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
 
-    v4i acc[4][4];
+    v4i acc[MI][MI];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4i{};
-    auto read_frags = [&](v4i (&a)[4], v4i (&b)[4], int buf, int s) __attribute__((always_inline)) {
-        const int8_t *la = lds + buf * t128::kStageBytes;
-        const int8_t *lb = la + t128::kTileBytes;
+        for (int ni = 0; ni < MI; ++ni) acc[mi][ni] = v4i{};
+    auto read_frags = [&](v4i (&a)[MI], v4i (&b)[MI], int buf, int s) __attribute__((always_inline)) {
+        const int8_t *la = lds + buf * T_::kStageBytes;
+        const int8_t *lb = la + T_::kTileBytes;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[s]);
+        for (int ni = 0; ni < MI; ++ni) b[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[s]);
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[s]);
+        for (int mi = 0; mi < MI; ++mi) a[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[s]);
     };
-    auto mfmas = [&](const v4i (&a)[4], const v4i (&b)[4]) __attribute__((always_inline)) {
+    auto mfmas = [&](const v4i (&a)[MI], const v4i (&b)[MI]) __attribute__((always_inline)) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < MI; ++ni)
                 acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
 
-    v4i a0[4], b0[4], a1[4], b1[4];
+    v4i a0[MI], b0[MI], a1[MI], b1[MI];
     stage(kt0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -605,45 +618,44 @@ __global__ __launch_bounds__(t128::kThreads, 2) void gemm_i8_t128(GemmArgs p) {
     }
 
     if (S > 1 &&
-        !splitk_combine<4, 4, 4>(p, reinterpret_cast<unsigned *>(lds + t128::kLdsBytes + 1536), acc, tile, slice, S, wave,
-                                 lane, tid))
+        !splitk_combine<MI, MI, 4>(p, reinterpret_cast<unsigned *>(lds + T_::kLdsBytes + 3 * TB * 4), acc, tile, slice, S,
+                                   wave, lane, tid))
         return;
 
-    // epilogue: the whole fp32 tile through LDS, then 512-B row stores
-    const int gi0 = tm * t128::TB, gj0 = tn * t128::TB;
-    float *sCx = reinterpret_cast<float *>(lds + t128::kLdsBytes);
-    float *sCw = sCx + t128::TB;
-    float *sB = sCw + t128::TB;
+    // epilogue: the whole fp32 tile through LDS, then row stores (TB/4 lanes of 16 B per row)
+    const int gi0 = tm * TB, gj0 = tn * TB;
+    float *sCx = reinterpret_cast<float *>(lds + T_::kLdsBytes);
+    float *sCw = sCx + TB;
+    float *sB = sCw + TB;
     __syncthreads();  // every wave is done with the staging ring
-    if (tid < t128::TB) sCx[tid] = p.Cx[gi0 + tid];
-    else sCw[tid - t128::TB] = p.Cw[gj0 + tid - t128::TB];
+    if (tid < TB) sCx[tid] = p.Cx[gi0 + tid];
+    else if (tid < 2 * TB) sCw[tid - TB] = p.Cw[gj0 + tid - TB];
     if constexpr (kEpi >= kEpiBias)
-        if (tid < t128::TB) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
+        if (tid < TB) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
     __syncthreads();
-    float *T = reinterpret_cast<float *>(lds);  // [128][128] fp32 = the 64-KiB ring
+    float *T = reinterpret_cast<float *>(lds);  // [TB][TB] fp32 in the ring
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-        const int jl = wn * 64 + ni * 16 + lrow;
+    for (int ni = 0; ni < MI; ++ni) {
+        const int jl = wn * WT + ni * 16 + lrow;
         const float cw = sCw[jl];
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int il = wm * 64 + mi * 16 + 4 * kq + r;
-                T[il * t128::TB + jl] = epi_extra<kEpi>(dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2), sB,
-                                                  jl);
+                const int il = wm * WT + mi * 16 + 4 * kq + r;
+                T[il * TB + jl] = epi_extra<kEpi>(dequantize(acc[mi][ni][r], outer_product(sCx[il], cw), p.inv_r2), sB, jl);
             }
     }
     __syncthreads();
     float *C = static_cast<float *>(p.C);
-    const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
-                      gj0 + t128::TB <= p.n;
-    const int c4 = (tid & 31) * 4;
+    const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) && gj0 + TB <= p.n;
+    constexpr int kLanesPerRow = TB / 4;
+    const int c4 = (tid % kLanesPerRow) * 4;
 #pragma unroll 4
-    for (int rr = tid >> 5; rr < t128::TB; rr += t128::kThreads / 32) {
+    for (int rr = tid / kLanesPerRow; rr < TB; rr += T_::kThreads / kLanesPerRow) {
         const int i = gi0 + rr;
         if (i >= p.m) break;
-        const float4 v = *reinterpret_cast<const float4 *>(T + rr * t128::TB + c4);
+        const float4 v = *reinterpret_cast<const float4 *>(T + rr * TB + c4);
         const int j = gj0 + c4;
         if (full) {
             *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = v;

@@ -201,6 +201,58 @@ int main(int argc, char **argv) {
                clk[nb - 1], 256.0 * 4 * 2048 * clk[nb / 2] * 1e-3);
         return 0;
     }
+    // small mode: build/gemm_lab m n k rounds small -- the small-tile kernels (128 and 64) at split-K
+    // S = 1, 2, 4 on library-style scratch, interleaved rounds
+    if (only && std::string(only) == "small") {
+        unsigned *tick; int32_t *slabs;
+        CK(hipMalloc(&tick, 4096)); CK(hipMemset(tick, 0, 4096));
+        const int t64m = (int)(mp / 64), t64n = (int)(np_ / 64);
+        CK(hipMalloc(&slabs, (size_t)t64m * t64n * 8 * 64 * 64 * 4 + (size_t)(mp / 128) * (np_ / 128) * 8 * 128 * 128 * 4));
+        struct SV { const char *name; KernelFn fn; int TB, S; };
+        std::vector<SV> sv = {
+            {"t128_S1", gemm_i8_small<128>, 128, 1}, {"t128_S2", gemm_i8_small<128>, 128, 2},
+            {"t128_S4", gemm_i8_small<128>, 128, 4}, {"t64_S1", gemm_i8_small<64>, 64, 1},
+            {"t64_S2", gemm_i8_small<64>, 64, 2}, {"t64_S4", gemm_i8_small<64>, 64, 4},
+        };
+        auto args = [&](const SV &v, float *out) {
+            GemmArgs q = p; q.C = out; q.splits = v.S; q.slabs = slabs; q.tickets = tick; q.reset_tickets = 1;
+            q.tiles_m = (int)(mp / v.TB); q.tiles_n = (int)(np_ / v.TB);
+            return q;
+        };
+        auto grid_of = [&](const SV &v) { return dim3((unsigned)((mp / v.TB) * (np_ / v.TB) * v.S)); };
+        std::vector<float> h1((size_t)m * n), h2((size_t)m * n);
+        sv[0].fn<<<grid_of(sv[0]), 256>>>(args(sv[0], Cref));
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h1.data(), Cref, h1.size() * 4, hipMemcpyDeviceToHost));
+        for (auto &v : sv) {
+            if ((int64_t)(k / 128) / v.S < 1) continue;
+            CK(hipMemset(C, 0xff, (size_t)m * n * 4));
+            v.fn<<<grid_of(v), 256>>>(args(v, C));
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(h2.data(), C, h2.size() * 4, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t i = 0; i < h1.size(); ++i) bad += memcmp(&h1[i], &h2[i], 4) != 0;
+            printf("check %-8s mismatches %zu\n", v.name, bad);
+        }
+        hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        std::vector<std::vector<float>> t(sv.size());
+        for (int r = 0; r < std::max(rounds, 3); ++r)
+            for (size_t vi = 0; vi < sv.size(); ++vi) {
+                const GemmArgs q = args(sv[vi], C);
+                const dim3 g = grid_of(sv[vi]);
+                for (int w = 0; w < 3; ++w) sv[vi].fn<<<g, 256>>>(q);
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < reps; ++i) sv[vi].fn<<<g, 256>>>(q);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                t[vi].push_back(ms * 1000 / reps);
+            }
+        for (size_t vi = 0; vi < sv.size(); ++vi) {
+            auto v = t[vi]; std::sort(v.begin(), v.end());
+            printf("%-8s median %8.2f us  min %8.2f us  (%u blocks)\n", sv[vi].name, v[v.size() / 2], v[0], grid_of(sv[vi]).x);
+        }
+        return 0;
+    }
     // split mode: build/gemm_lab m n k rounds split -- the product kernel at split-K S = 1, 2, 4 (and the
     // slab-free ablation: tickets only, wrong sums) on library-style scratch (tickets zeroed once,
     // reducers re-zero them), interleaved rounds

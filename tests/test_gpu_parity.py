@@ -98,7 +98,7 @@ def test_single_pass_8_column_strips(qg, oracle, device, M, N, K):
     _check_intermediates(qg, X, W, ref, device, f"{M}x{N}x{K}")
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 4096), (300, 520, 1000), (512, 1024, 2048)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 4096), (200, 300, 8192), (512, 1024, 4096), (300, 520, 1000)])
 def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
     """Few-tile shapes run split-K (int32 slabs + arrival tickets, combined in-launch): exact integer
     sums, so bit-identical to the oracle; repeated calls reuse the tickets (zeroed per launch) and
@@ -115,7 +115,7 @@ def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
     assert_bits_equal(_run_full(qg, X, W, device), want, f"{M}x{N}x{K} op_quantized_mm")
 
 
-@pytest.mark.parametrize("M,N,K,layout", [(256, 256, 4096, "rows"), (300, 520, 4500, "rows"), (256, 512, 2048, "rows"),
+@pytest.mark.parametrize("M,N,K,layout", [(256, 256, 4096, "rows"), (300, 520, 4500, "rows"), (256, 512, 4096, "rows"),
                                           (256, 256, 4096, "generic")])
 def test_split_k_poisoned_caller_workspace(qg, oracle, device, M, N, K, layout):
     """op_mm_quantize_ws on a workspace full of 0xFF at split-K shapes: the split-K tickets at its start
@@ -145,7 +145,7 @@ def test_split_k_poisoned_caller_workspace(qg, oracle, device, M, N, K, layout):
 def test_split_k_shapes_share_library_scratch(qg, oracle, device):
     """Different split-K plans one after another on the same stream share qgemm_mm_packed's scratch
     (tickets zeroed once, re-zeroed by each launch's reducers): every call stays bit-exact."""
-    shapes = [(512, 3072, 1024), (512, 1024, 4096), (256, 256, 2048), (512, 3072, 1024), (512, 1024, 4096)]
+    shapes = [(512, 1024, 4096), (64, 512, 8192), (256, 256, 4096), (512, 3072, 1024), (512, 1024, 4096), (64, 512, 8192)]
     cache = {}
     for i, (M, N, K) in enumerate(shapes):
         if (M, N, K) not in cache:
