@@ -20,22 +20,30 @@ namespace {
 constexpr int kRowWaves = 4;       // rows per 256-thread block
 constexpr int kMaxRowLen = 4096;   // LDS staging per wave: 16 KiB
 
-// sequential fp32 sum of row[0..w) in element order (every lane computes the same chain)
-__device__ __forceinline__ float seq_sum(const float *row, int w) {
-    float sum = 0.0f;
-    int e = 0;
-    for (; e + 16 <= w; e += 16) {
-        float4 q[4];
+// sequential fp32 sum of row[0..w) in element order (every lane computes the same chain; the reads
+// are LDS broadcasts).  The chain is latency-bound: groups of G elements are read with G/4 b128 loads
+// issued together, so each group waits out the LDS latency once (G = 64: 4x fewer exposed latencies
+// than groups of 16), then the 16-element and scalar tails.
+template <int G>
+__device__ __forceinline__ void seq_sum_groups(const float *row, int w, int &e, float &sum) {
+    for (; e + G <= w; e += G) {
+        float4 q[G / 4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(row + e + 4 * j);
+        for (int j = 0; j < G / 4; ++j) q[j] = *reinterpret_cast<const float4 *>(row + e + 4 * j);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < G / 4; ++j) {
             sum = __fadd_rn(sum, q[j].x);
             sum = __fadd_rn(sum, q[j].y);
             sum = __fadd_rn(sum, q[j].z);
             sum = __fadd_rn(sum, q[j].w);
         }
     }
+}
+__device__ __forceinline__ float seq_sum(const float *row, int w) {
+    float sum = 0.0f;
+    int e = 0;
+    seq_sum_groups<64>(row, w, e, sum);
+    seq_sum_groups<16>(row, w, e, sum);
     for (; e < w; ++e) sum = __fadd_rn(sum, row[e]);
     return sum;
 }
