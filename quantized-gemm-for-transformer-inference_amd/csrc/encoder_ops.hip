@@ -48,6 +48,12 @@ __device__ __forceinline__ float seq_sum(const float *row, int w) {
     return sum;
 }
 
+// fl((x - mean)^2): pow(x - mean, 2) as fp32 d*d (CUDA's float pow(float, int) overload)
+__device__ __forceinline__ float sq_dev(float x, float mean) {
+    const float d = __fsub_rn(x, mean);
+    return __fmul_rn(d, d);
+}
+
 __global__ __launch_bounds__(64 * kRowWaves) void softmax_rows_kernel(const float *S, float *P, int64_t rows, int w,
                                                                       float scale) {  // P may be S (in place)
     extern __shared__ __attribute__((aligned(16))) float stage[];
@@ -85,7 +91,9 @@ __global__ __launch_bounds__(64 * kRowWaves) void softmax_rows_kernel(const floa
 // s = fl(range / Cx), q = sat_i8(trunc(fl(y * s))) -- the same operations as pack_rows_vec_body, so
 // the packed row is bit-identical to packing Y afterwards.  Rows [rows, rows_pad) of the packed view
 // get zero bytes and a zero scale; columns [w, k_pad) zero bytes.
-template <bool kPack>
+// kStamp (lab only; 0 in the library): s_memrealtime stamps at the phase boundaries (g_ln_stamp)
+__device__ unsigned long long g_ln_stamp[4096][8];
+template <bool kPack, int kStamp = 0>
 __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(const float *__restrict__ A,
                                                                             const float *__restrict__ B,
                                                                             float *__restrict__ Y, int64_t rows,
@@ -96,6 +104,11 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
     extern __shared__ __attribute__((aligned(16))) float stage[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (kStamp != 0)
+            if (lane == 0 && row < 4096) g_ln_stamp[row][i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     if (kPack && row >= rows && row < rows_pad) {  // padding row of the packed view
         uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
         for (int64_t c = lane; c < k_pad / 4; c += 64) qrow[c] = 0u;
@@ -109,17 +122,20 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
     for (int c = lane; c < w; c += 64) st[c] = __fadd_rn(a[c], b[c]);  // op_add (transformer.cu:58)
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    stamp(1);
     const float fw = (float)w;                                 // "mean/w": int -> float
     const float mean = __fdiv_rn(seq_sum(st, w), fw);          // op_layernorm.cuh:15-19
+    stamp(2);
     __builtin_amdgcn_wave_barrier();
     // the squared deviations replace the row in LDS (each lane rewrites the columns it owns)
     for (int c = lane; c < w; c += 64) {
-        const float d = __fsub_rn(st[c], mean);
-        st[c] = __fmul_rn(d, d);                               // pow(x - mean, 2) as fp32 d*d
+        st[c] = sq_dev(st[c], mean);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    stamp(3);
     const float var = __fdiv_rn(seq_sum(st, w), fw);           // :21-25
+    stamp(4);
     float cand = -INFINITY;
     __builtin_amdgcn_wave_barrier();
     for (int c = lane; c < w; c += 64) {                       // (x - mean) / var (:28), as written
@@ -130,6 +146,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
             if (c > 0) cand = fmaxf(cand, absmax_candidate(v));
         }
     }
+    stamp(5);
     if constexpr (kPack) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) cand = fmaxf(cand, __shfl_xor(cand, off, 64));
@@ -147,6 +164,130 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
         }
         if (lane == 0) qscale[row] = cx;
     }
+    stamp(6);
+}
+
+// The same add + layernorm (+ pack) for rows of w % 4 == 0 floats, 16-B aligned: each lane holds its
+// columns 4j..4j+3 (j = lane + 64 i, i < kV) in registers from the first load to the last use, so
+// neither the normalisation nor the pack re-reads A, B or LDS; each packed dword is
+// one lane's four columns.
+template <bool kPack, int kV, int kStamp = 0>
+__global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
+    const float *__restrict__ A, const float *__restrict__ B, float *__restrict__ Y, int64_t rows, int w,
+    int8_t *__restrict__ q, float *__restrict__ qscale, int64_t k_pad, int64_t rows_pad, float range) {
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (kStamp != 0)
+            if (lane == 0 && row < 4096) g_ln_stamp[row][i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
+    if (kPack && row >= rows && row < rows_pad) {  // padding row of the packed view
+        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+        for (int64_t c = lane; c < k_pad / 4; c += 64) qrow[c] = 0u;
+        if (lane == 0) qscale[row] = 0.0f;
+        return;
+    }
+    if (row >= rows) return;
+    const int w4 = w >> 2;
+    const float4 *a = reinterpret_cast<const float4 *>(A + row * w), *b = reinterpret_cast<const float4 *>(B + row * w);
+    float4 *y = reinterpret_cast<float4 *>(Y + row * w);
+    float *st = stage + wv * w;
+    float4 x[kV];
+#pragma unroll
+    for (int i = 0; i < kV; ++i) {
+        const int j = lane + 64 * i;
+        if (j < w4) {
+            const float4 av = a[j], bv = b[j];
+            x[i] = make_float4(__fadd_rn(av.x, bv.x), __fadd_rn(av.y, bv.y), __fadd_rn(av.z, bv.z),
+                               __fadd_rn(av.w, bv.w));  // op_add (transformer.cu:58)
+            reinterpret_cast<float4 *>(st)[j] = x[i];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    stamp(1);
+    const float fw = (float)w;
+    const float mean = __fdiv_rn(seq_sum(st, w), fw);           // op_layernorm.cuh:15-19
+    stamp(2);
+    __builtin_amdgcn_wave_barrier();
+    // the squared deviations replace the row in LDS, formed from the registers (a chain that formed
+    // them itself would carry the sub -> mul latency on every add: measured 2x slower)
+#pragma unroll
+    for (int i = 0; i < kV; ++i) {
+        const int j = lane + 64 * i;
+        if (j < w4)
+            reinterpret_cast<float4 *>(st)[j] =
+                make_float4(sq_dev(x[i].x, mean), sq_dev(x[i].y, mean), sq_dev(x[i].z, mean), sq_dev(x[i].w, mean));
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    stamp(3);
+    const float var = __fdiv_rn(seq_sum(st, w), fw);            // :21-25
+    stamp(4);
+    float cand = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < kV; ++i) {
+        const int j = lane + 64 * i;
+        if (j < w4) {
+            float4 v;                                                // (x - mean) / var (:28), as written
+            v.x = __fdiv_rn(__fsub_rn(x[i].x, mean), var);
+            v.y = __fdiv_rn(__fsub_rn(x[i].y, mean), var);
+            v.z = __fdiv_rn(__fsub_rn(x[i].z, mean), var);
+            v.w = __fdiv_rn(__fsub_rn(x[i].w, mean), var);
+            y[j] = v;
+            x[i] = v;
+            if constexpr (kPack) {
+                if (j > 0) cand = fmaxf(cand, absmax_candidate(v.x));
+                cand = fmaxf(cand, absmax_candidate(v.y));
+                cand = fmaxf(cand, absmax_candidate(v.z));
+                cand = fmaxf(cand, absmax_candidate(v.w));
+            }
+        }
+    }
+    stamp(5);
+    if constexpr (kPack) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) cand = fmaxf(cand, __shfl_xor(cand, off, 64));
+        const float seed = __shfl(x[0].x, 0, 64);  // column 0: lane 0, i = 0
+        const float cx = absmax_finish(seed, cand);
+        const float sc = inv_divide(range, cx);
+        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+#pragma unroll
+        for (int i = 0; i < kV; ++i) {
+            const int j = lane + 64 * i;
+            if (j < w4)
+                qrow[j] = (uint32_t)(quant_i8(x[i].x, sc) & 0xff) | ((uint32_t)(quant_i8(x[i].y, sc) & 0xff) << 8) |
+                          ((uint32_t)(quant_i8(x[i].z, sc) & 0xff) << 16) | ((uint32_t)(quant_i8(x[i].w, sc) & 0xff) << 24);
+        }
+        for (int64_t c4 = w4 + lane; c4 < k_pad / 4; c4 += 64) qrow[c4] = 0u;  // padding columns
+        if (lane == 0) qscale[row] = cx;
+    }
+    stamp(6);
+}
+
+// register-resident path: w % 4 == 0, w <= 256 * kV (kV = 4, 8 or 16), 16-B aligned rows
+template <bool kPack>
+hipError_t launch_ln_vec(const float *A, const float *B, float *Y, int64_t rows, int w, int8_t *q, float *qscale,
+                         int64_t k_pad, int64_t rows_pad, float range, int64_t grid_rows, hipStream_t stream) {
+    const size_t lds = sizeof(float) * kRowWaves * w;
+    const unsigned grid = (unsigned)((grid_rows + kRowWaves - 1) / kRowWaves);
+    if (w <= 1024)
+        add_layernorm_rows_vec_kernel<kPack, 4><<<grid, 64 * kRowWaves, lds, stream>>>(A, B, Y, rows, w, q, qscale, k_pad,
+                                                                                      rows_pad, range);
+    else if (w <= 2048)
+        add_layernorm_rows_vec_kernel<kPack, 8><<<grid, 64 * kRowWaves, lds, stream>>>(A, B, Y, rows, w, q, qscale, k_pad,
+                                                                                      rows_pad, range);
+    else
+        add_layernorm_rows_vec_kernel<kPack, 16><<<grid, 64 * kRowWaves, lds, stream>>>(A, B, Y, rows, w, q, qscale,
+                                                                                       k_pad, rows_pad, range);
+    return hipGetLastError();
+}
+
+bool ln_vec_ok(const float *A, const float *B, const float *Y, int w) {
+    const uintptr_t al = reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(Y);
+    return w % 4 == 0 && w <= kMaxRowLen && (al & 15) == 0;
 }
 
 }  // namespace
@@ -164,6 +305,7 @@ hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, i
                                      hipStream_t stream) {
     if (w < 1 || w > kMaxRowLen || rows < 0) return hipErrorInvalidValue;
     if (rows == 0) return hipSuccess;
+    if (ln_vec_ok(A, B, Y, w)) return launch_ln_vec<false>(A, B, Y, rows, w, nullptr, nullptr, 0, 0, 0.0f, rows, stream);
     const size_t lds = sizeof(float) * kRowWaves * ((w + 3) & ~3);
     add_layernorm_rows_kernel<false><<<(unsigned)((rows + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds, stream>>>(
         A, B, Y, rows, w, nullptr, nullptr, 0, 0, 0.0f);
@@ -173,6 +315,8 @@ hipError_t launch_add_layernorm_rows(const float *A, const float *B, float *Y, i
 hipError_t launch_add_layernorm_rows_pack(const float *A, const float *B, float *Y, int64_t rows, int w, float range,
                                           PackedView out, hipStream_t stream) {
     if (w < 1 || w > kMaxRowLen || rows < 1 || out.k_pad < w || out.rows_pad < rows) return hipErrorInvalidValue;
+    if (ln_vec_ok(A, B, Y, w))
+        return launch_ln_vec<true>(A, B, Y, rows, w, out.q, out.scale, out.k_pad, out.rows_pad, range, out.rows_pad, stream);
     const size_t lds = sizeof(float) * kRowWaves * ((w + 3) & ~3);
     add_layernorm_rows_kernel<true><<<(unsigned)((out.rows_pad + kRowWaves - 1) / kRowWaves), 64 * kRowWaves, lds,
                                       stream>>>(A, B, Y, rows, w, out.q, out.scale, out.k_pad, out.rows_pad, range);

@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 #include "../csrc/encoder_ops.hip"
 
@@ -64,6 +65,56 @@ int main(int argc, char **argv) {
         size_t br = 0;
         for (int r = 0; r < rows; ++r) br += memcmp(&h2[(size_t)r * w], &hy[(size_t)r * w], (size_t)w * 4) != 0;
         badruns += br > 0; badrows += br;
+    }
+    // the scalar (general) kernel against the register-resident one the launchers picked
+    {
+        PackedView v = packed_view(pk, rows, w);
+        void *pk2; float *Y3; CK(hipMalloc(&pk2, packed_bytes(rows, w))); CK(hipMalloc(&Y3, (size_t)rows * w * 4));
+        PackedView v2 = packed_view(pk2, rows, w);
+        CK(launch_add_layernorm_rows_pack(A, B, Y2, rows, w, 127.0f, v, nullptr));
+        const size_t lds = sizeof(float) * 4 * ((w + 3) & ~3);
+        add_layernorm_rows_kernel<true><<<(unsigned)((v2.rows_pad + 3) / 4), 256, lds>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+        CK(hipDeviceSynchronize());
+        auto same = [&](const void *x, const void *z, size_t n) {
+            std::vector<char> hx(n), hz(n);
+            CK(hipMemcpy(hx.data(), x, n, hipMemcpyDeviceToHost)); CK(hipMemcpy(hz.data(), z, n, hipMemcpyDeviceToHost));
+            return memcmp(hx.data(), hz.data(), n) == 0 ? "same" : "DIFF";
+        };
+        printf("vector vs scalar kernel: Y %s  q %s  scale %s\n", same(Y2, Y3, (size_t)rows * w * 4),
+               same(v.q, v2.q, v.rows_pad * v.k_pad), same(v.scale, v2.scale, v.rows_pad * 4));
+        hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        for (int var = 0; var < 2; ++var) {
+            std::vector<float> ts;
+            for (int it = 0; it < 30; ++it) {
+                CK(hipEventRecord(e0));
+                if (var == 0) CK(launch_add_layernorm_rows_pack(A, B, Y2, rows, w, 127.0f, v, nullptr));
+                else add_layernorm_rows_kernel<true><<<(unsigned)((v2.rows_pad + 3) / 4), 256, lds>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms * 1000);
+            }
+            std::sort(ts.begin(), ts.end());
+            printf("%s kernel: median %.2f us\n", var ? "scalar" : "vector", ts[ts.size() / 2]);
+        }
+    }
+    // phase stamps (s_memrealtime, 100 MHz) of the fused kernel, medians over rows
+    {
+        PackedView v = packed_view(pk, rows, w);
+        const size_t lds = sizeof(float) * 4 * ((w + 3) & ~3);
+        for (int it = 0; it < 5; ++it)
+            add_layernorm_rows_vec_kernel<true, 4, 1><<<(unsigned)((v.rows_pad + 3) / 4), 256, lds>>>(A, B, Y2, rows, w, v.q, v.scale, v.k_pad, v.rows_pad, 127.0f);
+        CK(hipDeviceSynchronize());
+        static unsigned long long st[4096][8];
+        CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_ln_stamp), sizeof(st)));
+        const char *names[6] = {"load a+b", "mean chain", "d^2 stage", "var chain", "y loop", "pack"};
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int r = 0; r < rows && r < 4096; ++r) { t0 = std::min(t0, st[r][0]); t1 = std::max(t1, st[r][6]); }
+        for (int ph = 0; ph < 6; ++ph) {
+            std::vector<double> d;
+            for (int r = 0; r < rows && r < 4096; ++r) d.push_back((st[r][ph + 1] - st[r][ph]) * 10.0 / 1000.0);
+            std::sort(d.begin(), d.end());
+            printf("  %-12s median %6.2f us  max %6.2f us\n", names[ph], d[d.size() / 2], d.back());
+        }
+        printf("  kernel span (first start to last end) %.2f us\n", (t1 - t0) * 10.0 / 1000.0);
     }
     printf("%d repeated fused launches: %zu runs with wrong rows, %zu wrong rows total\n", reps, badruns, badrows);
     return 0;
