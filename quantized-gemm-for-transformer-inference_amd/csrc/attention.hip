@@ -19,27 +19,39 @@ namespace qgemm {
 
 namespace {
 
-constexpr int kTQ = 32;                    // query rows per workgroup
 constexpr int kAttnMaxSeq = 512;
 constexpr int kAttnMaxDk = 64;
-constexpr int kAttnThreads = 1024;         // 16 waves: 4 per SIMD hide the LDS and exp latencies
 constexpr int kSStride = kAttnMaxSeq + 4;  // S row stride (floats): consecutive rows 4 banks apart
-constexpr int kChunk = 256;                // keys per K / V chunk staged in LDS
 constexpr int kKStride = 68;               // K chunk [key][d_k]: B-fragment reads (16 keys x 4 k) conflict-free
 constexpr int kVStride = 80;               // V chunk [key][d_k]: B-fragment reads (4 keys x 16 cols) conflict-free
-constexpr int kKVFloats = kChunk * kVStride;
 constexpr int kQStride = 68;               // Q tile [query][d_k]: A-fragment reads conflict-free
+
+// Tile configurations.  kTQ query rows per workgroup, kChunk keys per K / V chunk, one 16-column QK tile
+// per wave (kChunk = 16 x waves), two softmax rows per wave (kTQ = 2 x waves).
+//   <32, 256, 1024>: 153 KiB of LDS, one workgroup per CU (the library's choice);
+//   <16, 128, 512> : 77 KiB, two workgroups per CU whose phases could overlap -- measured slower
+//                    (36.5 vs 30.6 us at config 5: twice the K / V staging, one QK chain per wave).
+template <int kTQ, int kChunk, int kThreads>
+struct AttnTile {
+    static constexpr int kWaves = kThreads / 64;
+    static_assert(kChunk == 16 * kWaves && kTQ == 2 * kWaves, "one QK column tile and two softmax rows per wave");
+    static constexpr int kRowFrags = kTQ / 16;
+    static constexpr int kKVFloats = kChunk * kVStride;
+    static constexpr int kWavesPerEu = 4;  // 4 waves per SIMD either way: <= 128 VGPRs
+};
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 // kSkip (lab ablation only; 0 in the library): 1 = no QK^T MFMAs, 2 = no softmax, 4 = no PV MFMAs,
 // 8 = no sequential sums, 16 = s_memrealtime stamps at the phase boundaries (g_attn_stamp)
-__device__ unsigned long long g_attn_stamp[4096][6];
-template <int kSkip = 0>
-__global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const float *__restrict__ qkv, int d, int dk,
-                                                                       int seq, float scale, float *__restrict__ heads) {
+__device__ unsigned long long g_attn_stamp[4096][8];
+template <int kTQ, int kChunk, int kThreads, int kSkip = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void attention_fused_kernel(
+    const float *__restrict__ qkv, int d, int dk, int seq, float scale, float *__restrict__ heads) {
+    using T = AttnTile<kTQ, kChunk, kThreads>;
+    constexpr int kAttnThreads = kThreads, kRF = T::kRowFrags;
     __shared__ __attribute__((aligned(16))) float S[kTQ * kSStride];
-    __shared__ __attribute__((aligned(16))) float KV[kKVFloats];
+    __shared__ __attribute__((aligned(16))) float KV[T::kKVFloats];
     __shared__ __attribute__((aligned(16))) float Qs[kTQ * kQStride];
     const int h = blockIdx.y, q0 = blockIdx.x * kTQ;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -48,6 +60,7 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
     const int lr = lane & 15, lk = lane >> 4;  // MFMA operand lane: row lr of the fragment, k offset lk
     const int rows = seq - q0 < kTQ ? seq - q0 : kTQ;
     const int nchunks = (seq + kChunk - 1) / kChunk;
+    const int seq32 = (seq + 31) & ~31;  // the reference's k extent for P V: seq zero-padded to its 32-wide tile
     const int dk4 = (dk + 3) >> 2;  // float4 columns of a K / V row (the last one zero-padded)
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     auto stamp = [&](int i) __attribute__((always_inline)) {
@@ -56,10 +69,14 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
     };
     stamp(0);
 
-    // stage keys [c0, c0 + 256) of K or V into KV ([key][stride], zero past seq and past d_k)
-    auto stage = [&](const float *src, int c0, int stride) __attribute__((always_inline)) {
-        for (int f = t; f < kChunk * 16; f += kAttnThreads) {
-            const int row = f >> 4, c4 = f & 15, j = c0 + row;
+    // K / V chunks as float4 pieces, kPer per thread, fetched into registers one chunk ahead -- chunk
+    // c+1's global loads are in flight under chunk c's MFMAs, V chunk 0's under the last QK chunk and
+    // the softmax -- then written to KV ([key][stride], zero past seq and past d_k)
+    constexpr int kPer = kChunk * 16 / kThreads;
+    auto fetch = [&](float4 (&r)[kPer], const float *src, int c0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int f = t + i * kThreads, row = f >> 4, c4 = f & 15, j = c0 + row;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (j < seq && c4 < dk4) {
                 const float *p = src + j * ld + 4 * c4;
@@ -72,7 +89,14 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
                     v.w = 4 * c4 + 3 < dk ? p[3] : 0.f;
                 }
             }
-            *reinterpret_cast<float4 *>(KV + row * stride + 4 * c4) = v;
+            r[i] = v;
+        }
+    };
+    auto put = [&](const float4 (&r)[kPer], int stride) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int f = t + i * kThreads;
+            *reinterpret_cast<float4 *>(KV + (f >> 4) * stride + 4 * (f & 15)) = r[i];
         }
     };
 
@@ -80,6 +104,8 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
     // both 16-row halves (one B fragment, two A fragments)
     const int ns = dk4;  // k-steps (<= 16)
     // the Q tile through LDS (coalesced row loads once per workgroup, not per wave), with K chunk 0
+    float4 pf[kPer];
+    fetch(pf, Kb, 0);
     for (int f = t; f < kTQ * 16; f += kAttnThreads) {
         const int row = f >> 4, c4 = f & 15, i = q0 + row;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -92,15 +118,17 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
         }
         *reinterpret_cast<float4 *>(Qs + row * kQStride + 4 * c4) = v;
     }
-    float qa[2][16];
+    float qa[kRF][16];
     const bool padk = (dk % 32) != 0;
     for (int c = 0; c < nchunks; ++c) {
         if (c) __syncthreads();  // every wave is done with the previous chunk
-        stage(Kb, c * kChunk, kKStride);
+        put(pf, kKStride);
         __syncthreads();
+        if (c + 1 < nchunks) fetch(pf, Kb, (c + 1) * kChunk);
+        else fetch(pf, Vb, 0);
         if (c == 0) {
 #pragma unroll
-            for (int rf = 0; rf < 2; ++rf)
+            for (int rf = 0; rf < kRF; ++rf)
 #pragma unroll
                 for (int s = 0; s < 16; ++s) qa[rf][s] = Qs[(rf * 16 + lr) * kQStride + 4 * s + lk];
             stamp(1);
@@ -108,28 +136,32 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
         const int col = c * kChunk + wave * 16 + lr;
         if (c * kChunk + wave * 16 < seq) {
             const float *krow = KV + (wave * 16 + lr) * kKStride + lk;
-            v4f a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+            v4f acc[kRF];
+#pragma unroll
+            for (int rf = 0; rf < kRF; ++rf) acc[rf] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < 16; ++s)
                 if (s < ns && !(kSkip & 1)) {  // wave-uniform: no zero k-steps past the padded d_k (-0 would become +0)
                     const float kb = krow[4 * s];
-                    a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[0][s], kb, a0, 0, 0, 0);
-                    a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[1][s], kb, a1, 0, 0, 0);
+#pragma unroll
+                    for (int rf = 0; rf < kRF; ++rf)
+                        acc[rf] = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[rf][s], kb, acc[rf], 0, 0, 0);
                 }
             if (col < seq) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    S[(4 * lk + r) * kSStride + col] = padk ? __fadd_rn(a0[r], 0.0f) : a0[r];
-                    S[(16 + 4 * lk + r) * kSStride + col] = padk ? __fadd_rn(a1[r], 0.0f) : a1[r];
-                }
+                for (int rf = 0; rf < kRF; ++rf)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        S[(rf * 16 + 4 * lk + r) * kSStride + col] = padk ? __fadd_rn(acc[rf][r], 0.0f) : acc[rf][r];
             }
         }
     }
     __syncthreads();
     stamp(2);
 
-    // ---- softmax of rows 2w and 2w+1: max and exp across the lanes; the two sequential sums at once
-    // (lanes 0 and 1); the division across the lanes
+    // ---- softmax of rows 2w and 2w+1: max and exp across the lanes, the two sequential sums at once
+    // (lanes 0 and 1), the division across the lanes -- all through the LDS row (keeping the scaled
+    // scores and exps in registers instead measured 1 us slower per launch)
     for (int rr = 0; rr < 2 && !(kSkip & 2); ++rr) {
         const int rl = wave * 2 + rr;
         if (rl >= rows) break;
@@ -150,66 +182,77 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's exps are in LDS
     __builtin_amdgcn_wave_barrier();
+    stamp(6);
     float sum = 0.0f;
     if (lane < 2 && wave * 2 + lane < rows && !(kSkip & 8)) {
         const float *srow = S + (wave * 2 + lane) * kSStride;
         int c = 0;
-        for (; c + 4 <= seq; c += 4) {
-            const float4 v = *reinterpret_cast<const float4 *>(srow + c);
-            sum = __fadd_rn(sum, v.x);
-            sum = __fadd_rn(sum, v.y);
-            sum = __fadd_rn(sum, v.z);
-            sum = __fadd_rn(sum, v.w);
+        for (; c + 64 <= seq; c += 64) {  // 16 LDS reads in flight per group of 64 adds
+            float4 v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = *reinterpret_cast<const float4 *>(srow + c + 4 * j);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                sum = __fadd_rn(sum, v[j].x);
+                sum = __fadd_rn(sum, v[j].y);
+                sum = __fadd_rn(sum, v[j].z);
+                sum = __fadd_rn(sum, v[j].w);
+            }
         }
         for (; c < seq; ++c) sum = __fadd_rn(sum, srow[c]);
     }
+    stamp(7);
     for (int rr = 0; rr < 2 && !(kSkip & 2); ++rr) {
         const int rl = wave * 2 + rr;
         const float srr = __shfl(sum, rr, 64);
         if (rl >= rows) break;
         float *srow = S + rl * kSStride;
         for (int c = lane; c < seq; c += 64) srow[c] = __fdiv_rn(srow[c], srr);
+        if (lane < seq32 - seq) srow[seq + lane] = 0.0f;  // P over the zero-padded k range (< 32 columns)
     }
 
-    // ---- heads = P V, one V chunk at a time: waves 0 .. 2*ceil(d_k/16)-1 own output tile (row half
-    // w & 1, column tile w >> 1) and carry its accumulator across the chunks (the k chain stays in order)
-    const int nct2 = (dk + 15) >> 4, nks = (seq + 3) >> 2;
-    const bool padj = (seq % 32) != 0;
-    const bool pv_wave = wave < 2 * nct2;
-    const int rf = wave & 1, ct = wave >> 1;
+    // ---- heads = P V, one V chunk at a time: waves 0 .. kRF*ceil(d_k/16)-1 own output tile (row
+    // fragment w % kRF, column tile w / kRF) and carry its accumulator across the chunks (the k chain
+    // stays in order)
+    const int nct2 = (dk + 15) >> 4, nks32 = seq32 >> 2;
+    const bool pv_wave = wave < kRF * nct2;
+    const int rf = wave % kRF, ct = wave / kRF;
     const int col = ct * 16 + lr;
     const float *prow = S + (rf * 16 + lr) * kSStride + lk;
     v4f acc = {0.f, 0.f, 0.f, 0.f};
     for (int c = 0; c < nchunks; ++c) {
         __syncthreads();  // P complete (c = 0) / the previous V chunk consumed
         if (c == 0) stamp(3);
-        stage(Vb, c * kChunk, kVStride);
+        put(pf, kVStride);
         __syncthreads();
         if (c == 0) stamp(4);
+        if (c + 1 < nchunks) fetch(pf, Vb, (c + 1) * kChunk);
         if (pv_wave && !(kSkip & 4)) {
-            // the chunk's k-steps in groups of 16: group g+1's operands are read from LDS while group g's
-            // MFMAs run (the accumulation chain itself stays in k order)
-            const int s_beg = c * (kChunk / 4), s_end = min(nks, (c + 1) * (kChunk / 4));
-            const float *vcol = KV + lk * kVStride + col;
-            auto read = [&](float (&pa)[16], float (&vb)[16], int s0) __attribute__((always_inline)) {
+            // k-steps over the reference's zero-padded extent (seq rounded up to 32: P and V are zero
+            // past seq, so those steps are its padded tile's +0 adds), in groups of 8 -- a whole number
+            // of groups per chunk, no per-step conditions; group g+1's operands are read from LDS while
+            // group g's MFMAs run (the accumulation chain itself stays in k order)
+            const int s_beg = c * (kChunk / 4), s_end = min(nks32, (c + 1) * (kChunk / 4));
+            const float *vcol = KV + (lk - c * kChunk) * kVStride + col;
+            auto read = [&](float (&pa)[8], float (&vb)[8], int s0) __attribute__((always_inline)) {
 #pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int s = s0 + u, j = 4 * s + lk;
-                    pa[u] = j < seq ? prow[4 * s] : 0.0f;  // S past seq is not written
-                    vb[u] = s < s_end ? vcol[(4 * s - c * kChunk) * kVStride] : 0.0f;
+                for (int u = 0; u < 8; ++u) {
+                    pa[u] = prow[4 * (s0 + u)];
+                    vb[u] = vcol[4 * (s0 + u) * kVStride];
                 }
             };
-            float pa0[16], vb0[16], pa1[16], vb1[16];
+            auto mfma8 = [&](const float (&pa)[8], const float (&vb)[8]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[u], vb[u], acc, 0, 0, 0);
+            };
+            float pa0[8], vb0[8], pa1[8], vb1[8];
             if (s_beg < s_end) read(pa0, vb0, s_beg);
-            for (int s0 = s_beg; s0 < s_end; s0 += 32) {
-                if (s0 + 16 < s_end) read(pa1, vb1, s0 + 16);
-#pragma unroll
-                for (int u = 0; u < 16; ++u)
-                    if (s0 + u < s_end) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[u], vb0[u], acc, 0, 0, 0);
-                if (s0 + 32 < s_end) read(pa0, vb0, s0 + 32);
-#pragma unroll
-                for (int u = 0; u < 16; ++u)
-                    if (s0 + 16 + u < s_end) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[u], vb1[u], acc, 0, 0, 0);
+            for (int s0 = s_beg; s0 < s_end; s0 += 16) {
+                const bool two = s0 + 8 < s_end;
+                if (two) read(pa1, vb1, s0 + 8);
+                mfma8(pa0, vb0);
+                if (s0 + 16 < s_end) read(pa0, vb0, s0 + 16);
+                if (two) mfma8(pa1, vb1);
             }
         }
     }
@@ -218,7 +261,7 @@ __global__ __launch_bounds__(kAttnThreads) void attention_fused_kernel(const flo
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int rl = rf * 16 + 4 * lk + r;
-            if (rl < rows) heads[(int64_t)(q0 + rl) * d + (int64_t)h * dk + col] = padj ? __fadd_rn(acc[r], 0.0f) : acc[r];
+            if (rl < rows) heads[(int64_t)(q0 + rl) * d + (int64_t)h * dk + col] = acc[r];
         }
     }
 }
@@ -230,7 +273,8 @@ hipError_t launch_attention_fused(const float *qkv, int seq, int d, int n_heads,
     if (n_heads < 1 || d % n_heads) return hipErrorInvalidValue;
     const int dk = d / n_heads;
     if (seq < 1 || seq > kAttnMaxSeq || dk > kAttnMaxDk) return hipErrorNotSupported;
-    attention_fused_kernel<0><<<dim3((unsigned)((seq + kTQ - 1) / kTQ), (unsigned)n_heads), kAttnThreads, 0, stream>>>(
+    constexpr int kTQ = 32;
+    attention_fused_kernel<kTQ, 256, 1024><<<dim3((unsigned)((seq + kTQ - 1) / kTQ), (unsigned)n_heads), 1024, 0, stream>>>(
         qkv, d, dk, seq, scale, heads);
     return hipGetLastError();
 }

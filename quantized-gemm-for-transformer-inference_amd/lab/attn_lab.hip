@@ -23,41 +23,67 @@ int main(int argc, char **argv) {
     fill_lab<<<1024, 256>>>(qkv, (int64_t)seq * 3 * d);
     const float scale = 1.0f / 8.0f;
     typedef void (*K)(const float *, int, int, int, float, float *);
-    struct V { const char *name; K k; };
-    std::vector<V> vs = {{"full", attention_fused_kernel<0>}, {"no_qk", attention_fused_kernel<1>},
-                         {"no_softmax", attention_fused_kernel<2 | 8>}, {"no_sums", attention_fused_kernel<8>},
-                         {"no_pv", attention_fused_kernel<4>}, {"nothing", attention_fused_kernel<15>}};
-    dim3 g((seq + 31) / 32, H);
+    struct V { const char *name; K k; int tq, threads; };
+    std::vector<V> vs = {{"t32 full", attention_fused_kernel<32, 256, 1024, 0>, 32, 1024},
+                         {"t16 full", attention_fused_kernel<16, 128, 512, 0>, 16, 512},
+                         {"t16 no_qk", attention_fused_kernel<16, 128, 512, 1>, 16, 512},
+                         {"t16 no_softmax", attention_fused_kernel<16, 128, 512, 2 | 8>, 16, 512},
+                         {"t16 no_sums", attention_fused_kernel<16, 128, 512, 8>, 16, 512},
+                         {"t16 no_pv", attention_fused_kernel<16, 128, 512, 4>, 16, 512},
+                         {"t16 nothing", attention_fused_kernel<16, 128, 512, 15>, 16, 512}};
+    // the two tile configurations must agree bit for bit
+    {
+        float *h2; CK(hipMalloc(&h2, (size_t)seq * d * 4));
+        vs[0].k<<<dim3((seq + 31) / 32, H), 1024>>>(qkv, d, dk, seq, scale, heads);
+        vs[1].k<<<dim3((seq + 15) / 16, H), 512>>>(qkv, d, dk, seq, scale, h2);
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned> x((size_t)seq * d), y((size_t)seq * d);
+        CK(hipMemcpy(x.data(), heads, x.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), h2, y.size() * 4, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t i = 0; i < x.size(); ++i) bad += x[i] != y[i];
+        printf("t16 vs t32 outputs: %zu of %zu differ\n", bad, x.size());
+    }
     hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < 7; ++r)
         for (size_t i = 0; i < vs.size(); ++i) {
-            for (int w = 0; w < 3; ++w) vs[i].k<<<g, kAttnThreads>>>(qkv, d, dk, seq, scale, heads);
+            const dim3 g((seq + vs[i].tq - 1) / vs[i].tq, H);
+            for (int w = 0; w < 3; ++w) vs[i].k<<<g, vs[i].threads>>>(qkv, d, dk, seq, scale, heads);
             CK(hipEventRecord(a));
-            for (int w = 0; w < 20; ++w) vs[i].k<<<g, kAttnThreads>>>(qkv, d, dk, seq, scale, heads);
+            for (int w = 0; w < 20; ++w) vs[i].k<<<g, vs[i].threads>>>(qkv, d, dk, seq, scale, heads);
             CK(hipEventRecord(z)); CK(hipEventSynchronize(z));
             float ms; CK(hipEventElapsedTime(&ms, a, z)); t[i].push_back(ms * 1000 / 20);
         }
     for (size_t i = 0; i < vs.size(); ++i) {
         auto v = t[i]; std::sort(v.begin(), v.end());
-        printf("%-12s median %8.2f us\n", vs[i].name, v[v.size() / 2]);
+        printf("%-16s median %8.2f us\n", vs[i].name, v[v.size() / 2]);
     }
+    const dim3 g((seq + 15) / 16, H);
     // phase stamps (block-median durations, 100 MHz ticks): Q loads + K chunk 0 staged | QK | softmax |
     // V chunk 0 staged | PV
-    for (int w = 0; w < 5; ++w) attention_fused_kernel<16><<<g, kAttnThreads>>>(qkv, d, dk, seq, scale, heads);
+    for (int w = 0; w < 5; ++w) attention_fused_kernel<16, 128, 512, 16><<<g, 512>>>(qkv, d, dk, seq, scale, heads);
     CK(hipDeviceSynchronize());
     const int nb = g.x * g.y;
-    std::vector<unsigned long long> st((size_t)4096 * 6);
+    std::vector<unsigned long long> st((size_t)4096 * 8);
     CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_attn_stamp), st.size() * 8));
     const char *nm[5] = {"stage K0 + Q", "QK", "softmax", "stage V0", "PV"};
     for (int ph = 0; ph < 5; ++ph) {
         std::vector<double> v;
-        for (int b = 0; b < nb; ++b) v.push_back((st[(size_t)b * 6 + ph + 1] - st[(size_t)b * 6 + ph]) * 0.01);
+        for (int b = 0; b < nb; ++b) v.push_back((st[(size_t)b * 8 + ph + 1] - st[(size_t)b * 8 + ph]) * 0.01);
         std::sort(v.begin(), v.end());
         printf("  %-14s median %6.2f us  max %6.2f us\n", nm[ph], v[v.size() / 2], v.back());
     }
+    const int sub[4][2] = {{2, 6}, {6, 7}, {7, 3}, {0, 0}};
+    const char *snm[3] = {"  max+exp", "  sums", "  div+sync"};
+    for (int q = 0; q < 3; ++q) {
+        std::vector<double> v;
+        for (int b = 0; b < nb; ++b) v.push_back((st[(size_t)b * 8 + sub[q][1]] - st[(size_t)b * 8 + sub[q][0]]) * 0.01);
+        std::sort(v.begin(), v.end());
+        printf("  %-14s median %6.2f us  max %6.2f us  (wave 0)\n", snm[q], v[v.size() / 2], v.back());
+    }
     std::vector<double> tot;
-    for (int b = 0; b < nb; ++b) tot.push_back((st[(size_t)b * 6 + 5] - st[(size_t)b * 6]) * 0.01);
+    for (int b = 0; b < nb; ++b) tot.push_back((st[(size_t)b * 8 + 5] - st[(size_t)b * 8]) * 0.01);
     std::sort(tot.begin(), tot.end());
     printf("  block total median %6.2f us  max %6.2f us\n", tot[tot.size() / 2], tot.back());
     return 0;

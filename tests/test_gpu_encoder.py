@@ -55,6 +55,8 @@ def test_linear_fused_bias_relu_bit_exact(qg, oracle, device, M, N, K, bias, rel
     (100, 256, 8, 512, 3),    # ragged seq, odd block count
     (257, 96, 3, 64, 1),      # fused attention: d_k 32 (no +0 step), a second 256-key chunk holding one key
     (40, 60, 5, 32, 2),       # d_k 12: k % 4 == 0, k % 32 != 0
+    (480, 128, 2, 64, 1),     # seq % 64 == 32: the last P V group of 8 k-steps stands alone
+    (33, 64, 1, 64, 1),       # one query row in the second tile; P V over 64 padded keys
     (300, 128, 1, 64, 1),     # d_k 128 > 64: the three-launch attention fallback
     (600, 64, 2, 64, 1),      # seq 600 > 512: fallback
 ])
