@@ -383,7 +383,7 @@ def bench_encoder(args, qg, L, dev, world, rank, distributed):
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_INT8_TOPS, 4),
             "traffic": None,
-            "kernel": "gemm_i8_small<64> (fused Q/K/V projection, 512 x 3072 x 1024)",
+            "kernel": "gemm_i8_small<64, 0, 3> (fused Q/K/V projection, 512 x 3072 x 1024)",
             "timing": f"hipExtLaunchKernel start/stop events on {len(timed)} of the {args.steps} timed forwards",
         },
         "library": qg.version(),

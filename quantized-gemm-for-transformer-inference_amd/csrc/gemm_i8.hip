@@ -107,16 +107,16 @@ static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     return e;
 }
 
-template <int TB, int kEpi>
+template <int TB, int kEpi, int kDepth>
 static hipError_t launch_small(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     const GemmEvents ev = take_gemm_events();
     if ((ev.start || ev.stop) && g_event_mode == 0) {
-        hipExtLaunchKernelGGL((gemm_i8_small<TB, kEpi>), grid, dim3(SmallTile<TB>::kThreads), 0, stream, ev.start,
-                              ev.stop, 0, p);
+        hipExtLaunchKernelGGL((gemm_i8_small<TB, kEpi, kDepth>), grid, dim3(SmallTile<TB, kDepth>::kThreads), 0, stream,
+                              ev.start, ev.stop, 0, p);
         return hipGetLastError();
     }
     if (ev.start) (void)hipEventRecord(ev.start, stream);
-    gemm_i8_small<TB, kEpi><<<grid, dim3(SmallTile<TB>::kThreads), 0, stream>>>(p);
+    gemm_i8_small<TB, kEpi, kDepth><<<grid, dim3(SmallTile<TB, kDepth>::kThreads), 0, stream>>>(p);
     hipError_t e = hipGetLastError();
     if (ev.stop) (void)hipEventRecord(ev.stop, stream);
     return e;
@@ -145,8 +145,15 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
     }
     const dim3 grid((unsigned)(tiles * p.splits));
     if (g.tile == 64) {
-        if (!bias) return launch_small<64, kEpiNone>(p, grid, stream);
-        return relu ? launch_small<64, kEpiBiasRelu>(p, grid, stream) : launch_small<64, kEpiBias>(p, grid, stream);
+        // at most two 64-tiles per CU: a 3-stage ring (two k-steps in flight, three blocks per CU); more
+        // tiles: the 2-stage ring, four blocks per CU (gemm_lab ... small, us: 512x1024x1024 6.10 -> 5.67,
+        // 512x1024x4096 S2 10.73 -> 9.91, 512x3072x1024 7.43 -> 7.20; 2048^3 18.1 -> 22.3 with 3 stages)
+        if (tiles <= 512) {
+            if (!bias) return launch_small<64, kEpiNone, 3>(p, grid, stream);
+            return relu ? launch_small<64, kEpiBiasRelu, 3>(p, grid, stream) : launch_small<64, kEpiBias, 3>(p, grid, stream);
+        }
+        if (!bias) return launch_small<64, kEpiNone, 2>(p, grid, stream);
+        return relu ? launch_small<64, kEpiBiasRelu, 2>(p, grid, stream) : launch_small<64, kEpiBias, 2>(p, grid, stream);
     }
     if (!bias) return launch_v3<kEpiNone>(p, grid, stream);
     return relu ? launch_v3<kEpiBiasRelu>(p, grid, stream) : launch_v3<kEpiBias>(p, grid, stream);

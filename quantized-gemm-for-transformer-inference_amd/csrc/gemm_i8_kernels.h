@@ -514,7 +514,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
 // schedule and split-K combine as gemm_i8_v3; the epilogue writes the whole TB x TB fp32 tile through
 // the ring at once.  TB = 128: 64-KiB ring, two blocks per CU; TB = 64: 32-KiB ring, four blocks per
 // CU -- four times the tiles, so shapes whose 128-tiles leave most CUs idle spread over the chip.
-template <int TB>
+// kDepth > 2: a kDepth-stage ring with kDepth - 1 k-steps in flight (each k-step then waits for the
+// OLDEST stage only): these few-k-step GEMMs are bound by the LDS-DMA round trip, not by the MFMAs.
+template <int TB, int kDepth = 2>
 struct SmallTile {
     static constexpr int kThreads = 256;
     static constexpr int WT = TB / 2;                // wave tile rows = cols
@@ -523,8 +525,9 @@ struct SmallTile {
     static constexpr int kPieces = kRowsPerWave / 8; // 1-KiB LDS-DMA pieces per operand per wave
     static constexpr int kTileBytes = TB * BK;
     static constexpr int kStageBytes = 2 * kTileBytes;
-    static constexpr int kLdsBytes = 2 * kStageBytes;
-    static constexpr int kMinBlocks = TB == 128 ? 2 : 4;
+    static constexpr int kLdsBytes = kDepth * kStageBytes;
+    static constexpr int kMinBlocks = TB == 128 || kDepth > 2 ? 2 : 4;
+    static constexpr int kLoadsPerStage = 2 * kPieces;  // LDS-DMA instructions per wave per stage (vmcnt)
     static_assert(TB * TB * 4 <= kLdsBytes, "epilogue image fits the ring");
 };
 namespace t128 {  // the 128-tile constants (launch shape)
@@ -532,9 +535,10 @@ constexpr int TB = 128;
 constexpr int kThreads = SmallTile<128>::kThreads;
 }  // namespace t128
 
-template <int TB, int kEpi = kEpiNone>
-__global__ __launch_bounds__(SmallTile<TB>::kThreads, SmallTile<TB>::kMinBlocks) void gemm_i8_small(GemmArgs p) {
-    using T_ = SmallTile<TB>;
+template <int TB, int kEpi = kEpiNone, int kDepth = 2>
+__global__ __launch_bounds__((SmallTile<TB, kDepth>::kThreads), (SmallTile<TB, kDepth>::kMinBlocks)) void gemm_i8_small(
+    GemmArgs p) {
+    using T_ = SmallTile<TB, kDepth>;
     constexpr int MI = T_::MI, WT = T_::WT, RPW = T_::kRowsPerWave, NP = T_::kPieces;
     __shared__ __attribute__((aligned(16))) int8_t lds[T_::kLdsBytes + 4 * TB * 4];  // + Cx, Cw, bias, flag
     const int tid = threadIdx.x, lane = tid & 63;
@@ -601,20 +605,39 @@ __global__ __launch_bounds__(SmallTile<TB>::kThreads, SmallTile<TB>::kMinBlocks)
     };
 
     v4i a0[MI], b0[MI], a1[MI], b1[MI];
-    stage(kt0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    read_frags(a0, b0, 0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        const bool more = kt + 1 < nk;
-        if (more) stage(kt0 + kt + 1, cur ^ 1);
-        read_frags(a1, b1, cur, 1);
-        mfmas(a0, b0);
+    if constexpr (kDepth == 2) {
+        stage(kt0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (more) read_frags(a0, b0, cur ^ 1, 0);
-        mfmas(a1, b1);
+        read_frags(a0, b0, 0, 0);
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            const bool more = kt + 1 < nk;
+            if (more) stage(kt0 + kt + 1, cur ^ 1);
+            read_frags(a1, b1, cur, 1);
+            mfmas(a0, b0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (more) read_frags(a0, b0, cur ^ 1, 0);
+            mfmas(a1, b1);
+        }
+    } else {
+        // kDepth - 1 stages in flight; k-steps past the slice re-load its last k-step (clamped), so every
+        // trip waits for exactly kDepth - 2 younger stages
+        const int last = kt0 + nk - 1;
+#pragma unroll
+        for (int s = 0; s < kDepth - 1; ++s) stage(min(kt0 + s, last), s);
+        for (int kt = 0; kt < nk; ++kt) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDepth - 2) * T_::kLoadsPerStage) : "memory");
+            __syncthreads();  // stage kt visible to every wave; every wave is done with stage kt - 1's slot
+            stage(min(kt0 + kt + kDepth - 1, last), (kt + kDepth - 1) % kDepth);
+            const int cur = kt % kDepth;
+            read_frags(a0, b0, cur, 0);
+            read_frags(a1, b1, cur, 1);
+            mfmas(a0, b0);
+            mfmas(a1, b1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped re-loads land before the ring is reused
     }
 
     if (S > 1 &&

@@ -213,6 +213,11 @@ int main(int argc, char **argv) {
             {"t128_S1", gemm_i8_small<128>, 128, 1}, {"t128_S2", gemm_i8_small<128>, 128, 2},
             {"t128_S4", gemm_i8_small<128>, 128, 4}, {"t64_S1", gemm_i8_small<64>, 64, 1},
             {"t64_S2", gemm_i8_small<64>, 64, 2}, {"t64_S4", gemm_i8_small<64>, 64, 4},
+            {"t64_S8", gemm_i8_small<64>, 64, 8},
+            {"t64d3_S1", gemm_i8_small<64, 0, 3>, 64, 1}, {"t64d3_S2", gemm_i8_small<64, 0, 3>, 64, 2},
+            {"t64d4_S1", gemm_i8_small<64, 0, 4>, 64, 1}, {"t64d4_S2", gemm_i8_small<64, 0, 4>, 64, 2},
+            {"t64d4_S4", gemm_i8_small<64, 0, 4>, 64, 4}, {"t64d6_S1", gemm_i8_small<64, 0, 6>, 64, 1},
+            {"t64d8_S1", gemm_i8_small<64, 0, 8>, 64, 1}, {"t64d8_S2", gemm_i8_small<64, 0, 8>, 64, 2},
         };
         auto args = [&](const SV &v, float *out) {
             GemmArgs q = p; q.C = out; q.splits = v.S; q.slabs = slabs; q.tickets = tick; q.reset_tickets = 1;
