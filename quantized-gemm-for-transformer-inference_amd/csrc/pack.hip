@@ -357,10 +357,11 @@ __device__ __forceinline__ void load_col_tile(float4 (&x)[2][4], const float *__
 
 // Block = 64 output rows (input columns) x kTilesPerBlock k-tiles of 128: the column scales are
 // computed once, and tile kt+1's loads are in flight while tile kt is quantized, transposed and
-// stored.  Grid: (rows_pad/64, ceil(k_pad/128 / kTilesPerBlock)).
-constexpr int kTilesPerBlock = 4;
+// stored.  Grid: (rows_pad/64, ceil(k_pad/128 / kTilesPerBlock)).  lab/pack3_lab.hip at 4096 x 16384
+// (FFN down W): 2 / 4 / 8 / 16 / 32 tiles per block 70.1 / 74.7 / 69.2 / 68.9 / 87.8 us.
+constexpr int kTilesPerBlock = 8;
 
-template <bool VEC>
+template <bool VEC, int kTPB = kTilesPerBlock>
 __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
                                                         float range, const uint32_t *__restrict__ partial,
                                                         int64_t parts, int64_t rows_pad, float *__restrict__ scale,
@@ -370,8 +371,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
     const int t = threadIdx.x;
     const int64_t n0 = (int64_t)blockIdx.x * kTc;
     const int64_t nkt = k_pad / kTk;
-    const int64_t kt0 = (int64_t)blockIdx.y * kTilesPerBlock;
-    const int64_t kt1 = min(nkt, kt0 + kTilesPerBlock);
+    const int64_t kt0 = (int64_t)blockIdx.y * kTPB;
+    const int64_t kt1 = min(nkt, kt0 + kTPB);
     const int col4 = t & 15;  // 4 input columns n0 + 4*col4 .. +3
     const int rg = t >> 4;    // rows k0 + 4*rg + 64*h + {0..3}
     const int64_t c = n0 + 4 * col4;

@@ -1,0 +1,78 @@
+// pack3_lab.hip -- development harness (not part of the library): the K > 4096 pack path (FFN down,
+// 2048 x 16384 -> 4096): the fused X-rows + W-column-max pass, each half alone, and pass 2 (column
+// scales, quantize, transpose) at several k-tiles per block, bit-compared.
+// Build: make -C .. pack3lab   Run: build/pack3_lab [m n k reps]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+#include <functional>
+#include <cstring>
+
+#include "../csrc/pack.hip"
+
+using namespace qgemm;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+template <int TPB>
+static void pass2(const float *W, int k, int n, PackedView vw, hipStream_t s) {
+    const dim3 g2((unsigned)(vw.rows_pad / kTc), (unsigned)((vw.k_pad / kTk + TPB - 1) / TPB));
+    pack_cols_kernel<true, TPB><<<g2, 256, 0, s>>>(W, n, k, n, 127.f, vw.scratch, vw.parts, vw.rows_pad, vw.scale, vw.q,
+                                                   vw.k_pad);
+}
+
+int main(int argc, char **argv) {
+    int m = argc > 1 ? atoi(argv[1]) : 2048, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 16384;
+    int reps = argc > 4 ? atoi(argv[4]) : 10;
+    float *X, *W; void *PX, *PW, *PW2;
+    CK(hipMalloc(&X, (size_t)m * k * 4)); CK(hipMalloc(&W, (size_t)k * n * 4));
+    CK(hipMalloc(&PX, packed_bytes(m, k))); CK(hipMalloc(&PW, packed_bytes(n, k))); CK(hipMalloc(&PW2, packed_bytes(n, k)));
+    CK(launch_fill_uniform(X, (int64_t)m * k, 11, -1.f, 1.f, nullptr));
+    CK(launch_fill_uniform(W, (int64_t)k * n, 12, -1.f, 1.f, nullptr));
+    PackedView vx = packed_view(PX, m, k), vw = packed_view(PW, n, k), vw2 = packed_view(PW2, n, k);
+    hipStream_t s0; CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+    auto fused = [&]() { CK(launch_pack_rows_and_colmax(X, k, m, k, vx, W, n, n, vw, 127.f, s0)); };
+    auto rows_only = [&]() { CK(launch_pack_rows(X, k, 1, m, k, 127.f, vx, s0)); };
+    auto colmax_only = [&]() {
+        const dim3 g1((unsigned)((n + kColBlock - 1) / kColBlock), (unsigned)vw.parts);
+        colmax_kernel<true><<<g1, 256, 0, s0>>>(W, n, k, n, vw.scratch, vw.rows_pad);
+    };
+    // the library's pass 2 writes vw; the variants write vw2 (same partials: copied below)
+    CK(hipMemset(PW2, 0x5a, packed_bytes(n, k)));
+    fused(); CK(launch_pack_cols_pass2(W, n, k, n, 127.f, vw, s0)); CK(hipStreamSynchronize(s0));
+    const size_t part_bytes = (size_t)vw.parts * vw.rows_pad * 4;
+    auto sync_partials = [&]() { CK(hipMemcpyAsync(vw2.scratch, vw.scratch, part_bytes, hipMemcpyDeviceToDevice, s0)); };
+    struct V { const char *name; std::function<void()> f; };
+    std::vector<V> vs = {{"fused_pass1", fused}, {"rows_only", rows_only}, {"colmax_only", colmax_only},
+                         {"pass2_tpb4", [&] { CK(launch_pack_cols_pass2(W, n, k, n, 127.f, vw, s0)); }},
+                         {"pass2_tpb2", [&] { pass2<2>(W, k, n, vw2, s0); }},
+                         {"pass2_tpb8", [&] { pass2<8>(W, k, n, vw2, s0); }},
+                         {"pass2_tpb16", [&] { pass2<16>(W, k, n, vw2, s0); }},
+                         {"pass2_tpb32", [&] { pass2<32>(W, k, n, vw2, s0); }},
+                         {"split_r_c", [&] { rows_only(); colmax_only(); }},
+                         {"split_c_r", [&] { colmax_only(); rows_only(); }}};
+    for (int v = 4; v < 8; ++v) {
+        sync_partials(); CK(hipMemsetAsync(vw2.q, 0x5a, vw2.rows_pad * vw2.k_pad, s0));
+        vs[v].f(); CK(hipStreamSynchronize(s0));
+        std::vector<char> a(vw.rows_pad * vw.k_pad), b(a.size());
+        CK(hipMemcpy(a.data(), vw.q, a.size(), hipMemcpyDeviceToHost)); CK(hipMemcpy(b.data(), vw2.q, b.size(), hipMemcpyDeviceToHost));
+        printf("%-12s q %s\n", vs[v].name, memcmp(a.data(), b.data(), a.size()) ? "DIFF" : "same");
+    }
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> t(vs.size());
+    for (int r = 0; r < 5; ++r)
+        for (size_t i = 0; i < vs.size(); ++i) {
+            vs[i].f(); vs[i].f();
+            CK(hipEventRecord(e0, s0));
+            for (int j = 0; j < reps; ++j) vs[i].f();
+            CK(hipEventRecord(e1, s0)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t[i].push_back(ms * 1000 / reps);
+        }
+    const double xb = 4.0 * m * k + (double)m * k, wb1 = 4.0 * k * n, wb2 = 4.0 * k * n + (double)k * n;
+    const double bytes[10] = {xb + wb1, xb, wb1, wb2, wb2, wb2, wb2, wb2, xb + wb1, xb + wb1};
+    for (size_t i = 0; i < vs.size(); ++i) {
+        auto v = t[i]; std::sort(v.begin(), v.end());
+        printf("%-12s median %8.2f us  (%.2f TB/s)\n", vs[i].name, v[v.size() / 2], bytes[i] / (v[v.size() / 2] * 1e-6) / 1e12);
+    }
+    return 0;
+}
