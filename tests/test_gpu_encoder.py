@@ -38,6 +38,19 @@ def test_add_layernorm_rows_bit_exact(qg, oracle, device, rows, w):
     assert_bits_equal(Y.cpu().numpy(), oracle.add_layernorm_rows(A, B), f"add+layernorm {rows}x{w}")
 
 
+def test_add_layernorm_rows_misaligned_rows(qg, oracle, device):
+    """Rows 4-byte aligned only (storage offset 1): the general kernel instead of the float4 one."""
+    rows, w = 40, 1024
+    A, B = oracle.uniform((rows, w), 7), oracle.uniform((rows, w), 8)
+    bufs = []
+    for X in (A, B):
+        buf = torch.zeros(rows * w + 1, dtype=torch.float32, device=device)
+        buf[1:] = torch.from_numpy(X.reshape(-1)).to(device)
+        bufs.append(buf[1:].view(rows, w))
+    Y = qg.add_layernorm_rows(bufs[0], bufs[1])
+    assert_bits_equal(Y.cpu().numpy(), oracle.add_layernorm_rows(A, B), "add+layernorm misaligned")
+
+
 @pytest.mark.parametrize("M,N,K,bias,relu", [(100, 260, 300, True, True), (100, 260, 300, True, False),
                                              (100, 260, 300, False, False), (512, 1024, 1024, True, True),
                                              (512, 4096, 1024, True, False)])
