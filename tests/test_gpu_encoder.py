@@ -31,7 +31,8 @@ def test_softmax_in_place(qg, oracle, device):
     assert_bits_equal(Sd.cpu().numpy(), oracle.softmax_rows(S, 0.125), "softmax in place")
 
 
-@pytest.mark.parametrize("rows,w", [(33, 8), (512, 1024), (7, 4096), (9, 100)])
+@pytest.mark.parametrize("rows,w", [(33, 8), (512, 1024), (7, 4096), (9, 100), (1, 4), (5, 2052), (3, 1028),
+                                    (64, 6)])
 def test_add_layernorm_rows_bit_exact(qg, oracle, device, rows, w):
     A, B = oracle.uniform((rows, w), 5), oracle.uniform((rows, w), 6)
     Y = qg.add_layernorm_rows(_dev(A, device), _dev(B, device))

@@ -98,6 +98,15 @@ def test_single_pass_8_column_strips(qg, oracle, device, M, N, K):
     _check_intermediates(qg, X, W, ref, device, f"{M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 64, 128), (100, 200, 256), (512, 512, 384), (512, 1024, 1024),
+                                   (512, 3072, 1024), (130, 70, 640), (512, 4096, 1024)])
+def test_small_tiles_three_stage_ring(qg, oracle, device, M, N, K):
+    """64-tile GEMM with the 3-stage LDS ring (<= 512 tiles): one, two and three k-steps (the prologue's
+    clamped re-loads of the last k-step), ragged M/N edges, and the encoder's linear shapes."""
+    X, W = oracle.inputs(M, N, K, 27)
+    assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 4096), (200, 300, 8192), (512, 1024, 4096), (300, 520, 1000)])
 def test_split_k_shapes_repeated(qg, oracle, device, M, N, K):
     """Few-tile shapes run split-K (int32 slabs + arrival tickets, combined in-launch): exact integer
