@@ -15,6 +15,8 @@
 // through LDS in 256-key chunks: 155 KiB in all); outside it the encoder runs the three kernels.
 #include "qgemm_internal.h"
 
+#include <type_traits>
+
 namespace qgemm {
 
 namespace {
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
 
     // ---- S[32][seq] = Q K^T, one K chunk at a time: wave w computes 16-column tile w of the chunk for
     // both 16-row halves (one B fragment, two A fragments)
-    const int ns = dk4;  // k-steps (<= 16)
+    const int ns32 = ((dk + 31) & ~31) >> 2;  // k-steps over d_k zero-padded to 32: 8 or 16
     // the Q tile through LDS (coalesced row loads once per workgroup, not per wave), with K chunk 0
     float4 pf[kPer];
     fetch(pf, Kb, 0);
@@ -119,7 +121,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
         *reinterpret_cast<float4 *>(Qs + row * kQStride + 4 * c4) = v;
     }
     float qa[kRF][16];
-    const bool padk = (dk % 32) != 0;
     for (int c = 0; c < nchunks; ++c) {
         if (c) __syncthreads();  // every wave is done with the previous chunk
         put(pf, kKStride);
@@ -139,20 +140,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
             v4f acc[kRF];
 #pragma unroll
             for (int rf = 0; rf < kRF; ++rf) acc[rf] = v4f{0.f, 0.f, 0.f, 0.f};
+            // k-steps over the reference's zero-padded extent (d_k rounded up to 32: Q and K are zero past
+            // d_k, so those steps are its padded tile's +0 adds) -- 8 or 16 steps with no per-step
+            // condition, the B fragments read together
+            auto steps = [&](auto kSteps) __attribute__((always_inline)) {
+                constexpr int kS = decltype(kSteps)::value;
+                float kb[kS];
 #pragma unroll
-            for (int s = 0; s < 16; ++s)
-                if (s < ns && !(kSkip & 1)) {  // wave-uniform: no zero k-steps past the padded d_k (-0 would become +0)
-                    const float kb = krow[4 * s];
+                for (int s = 0; s < kS; ++s) kb[s] = krow[4 * s];
+#pragma unroll
+                for (int s = 0; s < kS; ++s)
 #pragma unroll
                     for (int rf = 0; rf < kRF; ++rf)
-                        acc[rf] = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[rf][s], kb, acc[rf], 0, 0, 0);
-                }
+                        acc[rf] = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[rf][s], kb[s], acc[rf], 0, 0, 0);
+            };
+            if (!(kSkip & 1)) {
+                if (ns32 == 16) steps(std::integral_constant<int, 16>());
+                else steps(std::integral_constant<int, 8>());
+            }
             if (col < seq) {
 #pragma unroll
                 for (int rf = 0; rf < kRF; ++rf)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        S[(rf * 16 + 4 * lk + r) * kSStride + col] = padk ? __fadd_rn(acc[rf][r], 0.0f) : acc[rf][r];
+                    for (int r = 0; r < 4; ++r) S[(rf * 16 + 4 * lk + r) * kSStride + col] = acc[rf][r];
             }
         }
     }
