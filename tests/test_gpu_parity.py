@@ -151,6 +151,28 @@ def test_split_k_poisoned_caller_workspace(qg, oracle, device, M, N, K, layout):
         ws.fill_(255)
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 8196, 300), (33, 12288, 4096), (128, 16384, 1000), (5, 9000, 2049),
+                                   (300, 8704, 513)])
+def test_wide_w_pack_poisoned_workspace(qg, oracle, device, M, N, K):
+    """Wide W (n > 8192, 256 < K <= 4096, the FFN-up shape class) on a workspace full of 0xFF, twice:
+    16-column strips, n % 16 != 0 (8-column strips), K not a multiple of 128."""
+    X, W = oracle.inputs(M, N, K, 93)
+    want = oracle.quantized_mm(X, W)
+    L = qg.load()
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    ws = torch.full((L.op_mm_quantize_workspace_size(M, N, K),), 255, dtype=torch.uint8, device=device)
+    s = qg._stream(device)
+    for i in range(2):
+        O = torch.full((M, N), float("nan"), device=device)
+        rc = L.op_mm_quantize_ws(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, 127.0,
+                                 ws.data_ptr(), ws.numel(), s)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} call {i}")
+        ws.fill_(255)
+    assert_bits_equal(_run_full(qg, X, W, device), want, f"{M}x{N}x{K} op_quantized_mm")
+
+
 def test_split_k_shapes_share_library_scratch(qg, oracle, device):
     """Different split-K plans one after another on the same stream share qgemm_mm_packed's scratch
     (tickets zeroed once, re-zeroed by each launch's reducers): every call stays bit-exact."""
