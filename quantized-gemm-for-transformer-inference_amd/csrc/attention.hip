@@ -55,7 +55,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     __shared__ __attribute__((aligned(16))) float S[kTQ * kSStride];
     __shared__ __attribute__((aligned(16))) float KV[T::kKVFloats];
     __shared__ __attribute__((aligned(16))) float Qs[kTQ * kQStride];
-    const int h = blockIdx.y, q0 = blockIdx.x * kTQ;
+    // XCD-aware: blocks b, b+8, ... share an XCD; each XCD gets a contiguous range of (head, query tile)
+    // pairs, so a head's query tiles (and its K / V re-reads) stay in one L2
+    const int nwg = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xq = nwg >> 3, xr = nwg & 7, xc = lin & 7;
+    const int logical = (xc < xr ? xc * (xq + 1) : xr * (xq + 1) + (xc - xr) * xq) + (lin >> 3);
+    const int h = logical / gridDim.x, q0 = (logical - h * gridDim.x) * kTQ;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int64_t ld = 3 * (int64_t)d;
     const float *Qb = qkv + (int64_t)h * dk, *Kb = qkv + d + (int64_t)h * dk, *Vb = qkv + 2 * (int64_t)d + (int64_t)h * dk;
