@@ -32,7 +32,10 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 # gfx950 dense int8 MFMA peak: 256 CU x 4 SIMD x 2048 ops/clk (v_mfma_i32_32x32x32_i8: 65536 ops per
 # 32 cycles) x 2.4 GHz = 5.033e15 ops/s (MI355X_MICROARCH.md: i8 = 2x the bf16 2.5 PF dense rate).
-PRACTICAL_INT8_TOPS = 3400.0  # measured sustained bare-MFMA int8 rate
+# Sustained bare int8-MFMA rate (lab/pp_lab.hip `peak`: v_mfma_i32_16x16x64_i8 back to back, operands in
+# registers with no VALU in the loop, every CU, 2 s; PMC MFMA busy 0.957; profiles/r02_mfma_peak.txt):
+# the chip holds ~2.03-2.05 GHz under it.  The 32x32x32 form sustains only 3515 TOPS (1.72 GHz).
+PRACTICAL_INT8_TOPS = 4116.0
 PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12
 PEAK_HBM_GBS = 8000.0
 
@@ -268,12 +271,12 @@ def main():
             "traffic_unit": "bytes per launch (HBM + Infinity Cache fill, FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
             "alg_bytes": M * K + N * K + 4 * M * N + 4 * (M + N),
-            "kernel": "gemm_i8_v3<kStoreLds> (int8 16x16x64 MFMA GEMM + fused dequant epilogue)",
+            "kernel": "gemm_i8_pp<1> (int8 16x16x64 MFMA GEMM, ping-pong schedule, fused dequant epilogue)",
             "ceiling_measured": {
                 "value": PRACTICAL_INT8_TOPS, "frac": round(achieved / PRACTICAL_INT8_TOPS, 4),
-                "note": "bare v_mfma_i32_16x16x64_i8 issue on toggling register operands, every CU, 2 s sustained: "
-                        "the chip holds ~1.95 GHz, so this is the int8 rate it sustains (lab/gemm_lab.hip peak "
-                        "mode; DESIGN.md s5)"},
+                "note": "bare v_mfma_i32_16x16x64_i8 issue, operands in registers, no VALU in the loop, every CU, "
+                        "2 s sustained (PMC MFMA busy 0.957 at ~2.03 GHz held clock; lab/pp_lab.hip peak mode; "
+                        "profiles/r02_mfma_peak.txt)"},
             "timing": {"record": "hipEventRecord right before/after the GEMM launch (same stream)",
                        "ext": "hipExtLaunchKernel start/stop events on the GEMM launch",
                        "none": "not timed"}[args.gemm_timing] + f" on {len(timed)} of the {args.steps} timed steps",

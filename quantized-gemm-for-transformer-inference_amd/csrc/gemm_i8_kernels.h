@@ -508,6 +508,216 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// gemm_i8_pp: the 256 x 256 tile of gemm_i8_v3 on a PING-PONG schedule.  Waves w and w + 4 share a
+// SIMD (a workgroup's waves are dealt over the 4 SIMDs cyclically), so the block is split into a LEAD
+// half (waves 0-3: tile rows 0-127) and a LAG half (waves 4-7: rows 128-255) that runs one slot
+// behind.  A k-step is two slots separated by raw s_barriers; in every slot one wave of each SIMD
+// issues its 64 MFMAs (both 64-deep sub-steps, 1024 pipe cycles) while its partner stages and reads
+// ALL of its next k-step's fragments (24 ds_read_b128) -- the MFMA pipe never waits for the partner's
+// LDS-DMA issue, fragment reads or the barrier skew, which in v3 both waves of a SIMD pay together.
+//
+//   slot:     2t            2t+1          2t+2
+//   lead:     R(t)          M(t)          R(t+1) ...
+//   lag:      M(t-1)        R(t)          M(t)   ...
+//
+// 2-stage LDS ring (64 KiB stages).  Staging (kDma):
+//   0: the lead waves issue stage t+1 whole in R(t) (16 LDS-DMA pieces each) and wait for it after
+//      M(t) -- two slots of flight.
+//   1: the lead waves issue A of stage t+1 in R(t) (8 pieces); lag wave wn issues B rows
+//      [64wn, 64wn+64) of stage t+2 at the end of R(t), right after its own fragment reads of stage t
+//      retired (only waves wn and wn+4 read those rows: the lead one a slot earlier), and waits for
+//      B of stage t+1 with vmcnt(8) before the slot's barrier.
+// Every ds_read of a stage comes a barrier after the issuing wave's covering vmcnt; every LDS-DMA
+// into a slot comes after the barrier that follows the last reads of it (lgkmcnt(0) before each
+// R-slot barrier).  Barrier counts match: lead 1 + 2nk, lag 2 + 2nk - 1.
+// lab-only flags (kPP*): in-kernel stamps, ablations
+enum PPFlags { kPPStamp = 1, kPPNoDma = 2, kPPNoStore = 4 };
+#ifdef QGEMM_LAB
+__device__ unsigned long long g_pp_stamp[4096 * 6];
+#endif
+
+template <int kDma, int kEpi = kEpiNone, int kFlags = 0>
+__global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
+#ifdef QGEMM_LAB
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (kFlags & kPPStamp)
+            if (threadIdx.x == 0) {
+                g_pp_stamp[blockIdx.x * 6 + 2 * i] = __builtin_amdgcn_s_memtime();
+                g_pp_stamp[blockIdx.x * 6 + 2 * i + 1] = __builtin_amdgcn_s_memrealtime();
+            }
+    };
+#else
+    static_assert(kFlags == 0, "lab flags need QGEMM_LAB");
+    auto stamp = [](int) {};
+#endif
+    stamp(0);
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + (kEpi >= kEpiBias ? 3072 : 2048)];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const bool lead = wm == 0;
+    const int S = p.splits > 1 ? p.splits : 1;
+    const int wid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = wid / S, slice = wid - tile * S;
+    int tm, tn;
+    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
+    const int nk_all = (int)(p.k_pad / BK);
+    const int kt0 = slice * nk_all / S;
+    const int nk = (slice + 1) * nk_all / S - kt0;
+    const int64_t kp = p.k_pad;
+    const int8_t *Ablk = p.A + (int64_t)tm * BM * kp + (int64_t)kt0 * BK;
+    const int8_t *Bblk = p.B + (int64_t)tn * BN * kp + (int64_t)kt0 * BK;
+    // piece q (8 rows x 128 B, one wave instruction) of an operand: lane l writes LDS bytes 16l.. of
+    // rows 8q.., i.e. row 8q + (l>>3), slot l&7, which holds global chunk (l&7) ^ (4(q&1) + (l>>4))
+    uint32_t voff[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) voff[e] = (uint32_t)((lane >> 3) * kp) + ((((lane & 7) ^ (4 * e + (lane >> 4)))) << 4);
+    // wave-uniform part: 8 pieces starting at piece q0 of one operand, k-step kt, into LDS at dst
+    auto pieces8 = [&](const int8_t *blk, int q0, int kt, int8_t *dst) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int q = q0 + i;
+            __builtin_amdgcn_global_load_lds((const void *)(blk + (int64_t)q * 8 * kp + (int64_t)kt * BK + voff[i & 1]),
+                                             (void *)(dst + q * 8 * BK), 16, 0, 0);
+        }
+    };
+    auto stageA = [&](int kt, int buf) __attribute__((always_inline)) {
+        pieces8(Ablk, 8 * wn, kt, lds + buf * kStageBytes);
+    };
+    auto stageB = [&](int kt, int buf) __attribute__((always_inline)) {
+        pieces8(Bblk, 8 * wn, kt, lds + buf * kStageBytes + kTileBytes);
+    };
+
+    const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
+    const int a_row0 = (wm * 128 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    int off[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+
+    v4i acc[8][4];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4i{};
+    // R reads sub-step 0's fragments and sub-step 1's B fragments (64 VGPRs); sub-step 1's A
+    // fragments are read inside M, each into the registers of the sub-step-0 A fragment whose four
+    // MFMAs were just issued (LDS reads beside the wave's own MFMAs cost the pipe nothing; the
+    // 128 accumulators + fragments then fit 256 VGPRs without spills)
+    v4i a0[8], b0[4], b1[4];
+    auto read_r = [&](int buf) __attribute__((always_inline)) {
+        const int8_t *la = lds + buf * kStageBytes;
+        const int8_t *lb = la + kTileBytes;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b0[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[0]);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a0[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[0]);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b1[ni] = *reinterpret_cast<const v4i *>(lb + b_row0 + ni * 16 * BK + off[1]);
+    };
+    auto mfmas = [&](int buf) __attribute__((always_inline)) {
+        const int8_t *la = lds + buf * kStageBytes;
+        v4i a1[8];
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        // a1[mi] is read right after row mi's MFMAs (into a0[mi]'s registers); a1[7] goes out with
+        // a1[6], so the first sub-step-1 MFMA does not wait for a read issued after the last
+        // sub-step-0 MFMA
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0[mi], b0[ni], acc[mi][ni], 0, 0, 0);
+            if (mi < 6) a1[mi] = *reinterpret_cast<const v4i *>(la + a_row0 + mi * 16 * BK + off[1]);
+            if (mi == 6) {
+                a1[6] = *reinterpret_cast<const v4i *>(la + a_row0 + 6 * 16 * BK + off[1]);
+                a1[7] = *reinterpret_cast<const v4i *>(la + a_row0 + 7 * 16 * BK + off[1]);
+            }
+        }
+#pragma unroll
+        for (int mi = 0; mi < 6; ++mi) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1[mi], b1[ni], acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: stage 0 (+ B of stage 1 in mode 1) -> B0
+    if constexpr (kDma == 0) {
+        if (lead) {
+            stageA(0, 0);
+            stageB(0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        if (lead) {
+            stageA(0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            stageB(0, 0);
+            if (nk > 1) {
+                stageB(1, 1);
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+    }
+    barrier();
+    if (!lead) barrier();  // the lag half idles through slot 0
+    for (int t = 0; t < nk; ++t) {
+        const int cur = t & 1;
+        // ---- R(t)
+        if (lead && t + 1 < nk && (!(kFlags & kPPNoDma) || t == 0)) {
+            stageA(t + 1, cur ^ 1);
+            if constexpr (kDma == 0) stageB(t + 1, cur ^ 1);
+        }
+        read_r(cur);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (kDma == 1) {
+            if (!lead) {
+                if (t + 2 < nk && !(kFlags & kPPNoDma)) {
+                    stageB(t + 2, cur);
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            }
+        }
+        barrier();
+        // ---- M(t)
+        mfmas(cur);
+        if (lead) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier();
+        } else if (t + 1 < nk) {
+            barrier();
+        }
+    }
+
+    stamp(1);
+    if (S > 1 && !splitk_combine<8, 4, 8>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice, S, wave,
+                                          lane, tid))
+        return;
+    epilogue16<(kFlags & kPPNoStore) ? kStoreNone : kStoreLds, kEpi>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+    stamp(2);
+}
+
+// ------------------------------------------------------------------------------------------------
 // gemm_i8_small<TB>: TB x TB macro-tiles (TB = 128 or 64) for problems with few 256 x 256 tiles (the
 // encoder's M = 512 linears, decode-sized M): 4 waves as 2 x 2, each (TB/2) x (TB/2) = MI x MI tiles
 // of v_mfma_i32_16x16x64_i8, the same staging (LDS-DMA, source-swizzled 128-B rows, 2-deep ring),

@@ -18,7 +18,7 @@ run() { # name timeout cmd...
 STEPS="${STEPS:-pytest bench prof}"
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
