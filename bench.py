@@ -63,7 +63,9 @@ def parse():
     p.add_argument("--cold-steps", type=int, default=20,
                    help="after the timed region: calls timed one by one after a 1-GiB read sweep that evicts the "
                         "inputs from the 256-MB Infinity Cache (0 = skip); reported beside the warm steady state")
-    p.add_argument("--gather", action="store_true", help="also time the whole-node all-gather of C (N>1)")
+    p.add_argument("--node-reps", type=int, default=10,
+                   help="timed whole-node C4 steps (shard compute + RCCL all-gather, after 2 warm-up steps) for the "
+                        "c4_node report (0 = skip); c2 config only")
     p.add_argument("--gemm-timing-every", type=int, default=5,
                    help="time the GEMM kernel on every n-th timed step (events cost ~4 us per timed step)")
     p.add_argument("--gemm-timing", default="ext", choices=["record", "ext", "none"],
@@ -155,6 +157,73 @@ def cpu_baseline(M, N, K, target_s):
     }
 
 
+def c4_node(args, qg, dev, world, rank, distributed):
+    """BASELINE configs[3] as a whole-node figure: the global M = 65536 x 4096 x 4096 problem with M sharded
+    over the `world` ranks (op_mm_quantize_shard: per-rank pointer offsets into the full A and C), then the
+    in-place RCCL all-gather of C over xGMI (qgemm_allgather_rows, libqgemm_dist.so -- our own rccl.h call
+    site; the communicator's id travels over torch.distributed).  Warm: 2 untimed steps, then
+    args.node_reps steps, each bracketed by a barrier; per step the max over ranks of each phase, reported
+    as medians.  Kept OUT of `value` (the gather moves 1 GiB of C, ~10x the compute)."""
+    import statistics
+    import torch
+    import torch.distributed as dist
+    Mg, N, K = 65536, 4096, 4096
+    A = qg.fill_uniform(torch.empty((Mg, K), device=dev), seed=2 * 7)  # the same A on every rank
+    B = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 7 + 1)
+    C = torch.empty((Mg, N), device=dev)
+    uid = qg.Comm.unique_id() if rank == 0 else bytes(qg.COMM_ID_BYTES)
+    if distributed:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    comm = qg.Comm(world, rank, uid)
+    hip = HipEvents(3)
+    comp, gath = [], []
+    try:
+        for it in range(2 + args.node_reps):
+            if distributed:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            s = qg._stream(dev)
+            hip.hip.hipEventRecord(hip.ev[0], s)
+            qg.op_mm_quantize_shard(A, B, C, world, rank)
+            hip.hip.hipEventRecord(hip.ev[1], s)
+            comm.allgather_rows(C)
+            hip.hip.hipEventRecord(hip.ev[2], s)
+            t = torch.tensor([hip.elapsed_ms(hip.ev[0], hip.ev[1]), hip.elapsed_ms(hip.ev[1], hip.ev[2])],
+                             device=dev, dtype=torch.float64)
+            if distributed:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if it >= 2:
+                comp.append(float(t[0]))
+                gath.append(float(t[1]))
+        # every rank now holds the whole C: check one row of every shard against this rank's own call
+        m0, rows = qg.shard_rows(Mg, world, rank)
+        probe = [qg.shard_rows(Mg, world, r)[0] for r in range(world)]
+        Cref = torch.empty((len(probe), N), device=dev)
+        for i, r0 in enumerate(probe):
+            qg.op_mm_quantize(A[r0:r0 + 1].contiguous(), B, Cref[i:i + 1])
+        torch.cuda.synchronize(dev)
+        gathered_ok = bool(torch.equal(C[probe].view(torch.int32), Cref.view(torch.int32)))
+    finally:
+        comm.close()
+        hip.destroy()
+    cm, gm = statistics.median(comp), statistics.median(gath)
+    return {
+        "workload": f"BASELINE configs[3]: M={Mg} K=N={N} sharded over {world} GPU(s) ({Mg // world} rows each) + "
+                    "in-place RCCL all-gather of C (1 GiB) over xGMI",
+        "global_M": Mg, "N": N, "K": K, "world": world, "shard_rows": rows,
+        "reps": args.node_reps, "compute_ms_median": round(cm, 4), "allgather_ms_median": round(gm, 4),
+        "node_gemms_per_s_compute": round(1e3 / cm, 2),
+        "node_gemms_per_s_with_allgather": round(1e3 / (cm + gm), 2),
+        "node_tops_compute": round(2.0 * Mg * N * K / (cm * 1e-3) / 1e12, 1),
+        "allgather_GBps_recv_per_rank": round(Mg * N * 4 * (world - 1) / world / (gm * 1e-3) / 1e9, 1) if world > 1 else None,
+        "gathered_rows_match_one_gpu": gathered_ok,
+        "note": "the compute is a full drop-in call per rank on its row shard (pack + GEMM); world 1: the whole "
+                "65536-row problem on one GPU and a no-op gather",
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -223,17 +292,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, gemm_ms = float(t[0]), float(t[1])
 
-    gather_ms = None
-    if distributed and args.gather:
-        from importlib import import_module  # noqa: F401
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        g0 = time.perf_counter()
-        full = qg.shard.gather_rows(O, M * world)
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - g0) * 1e3
-        del full
-
     ops = 2.0 * M * N * K
     traffic, traffic_src = pmc_traffic(args.config)
     ms_per_step = elapsed * 1e3 / args.steps
@@ -283,8 +341,10 @@ def main():
         },
         "library": qg.version(),
     }
-    if gather_ms is not None:
-        result["allgather_C_ms"] = round(gather_ms, 3)
+    if args.config == "c2" and args.node_reps > 0:
+        node = c4_node(args, qg, dev, world, rank, distributed)
+        result["c4_node"] = node
+        result["allgather_ms_median"] = node["allgather_ms_median"]
     if rank == 0 and args.cold_steps > 0:
         # Steady-state steps re-read the same X and W, which (with O) fit in the 256-MB Infinity Cache;
         # this is the same call with them evicted first (a 1-GiB read sweep between calls), each call timed

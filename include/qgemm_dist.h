@@ -1,0 +1,68 @@
+/*
+ * qgemm_dist.h -- multi-GPU C-ABI of the quantized GEMM: M-sharding + RCCL all-gather over xGMI.
+ *
+ * The reference has no multi-GPU code; SURVEY.md s8(b) names the caller to serve ("the multi-GPU
+ * driver: per-rank pointer offsets A+m0*K, C+m0*N") and s8(e) the partitioning and collective
+ * (ncclAllGather of C, rccl.h:678).  The north star: "shard M across the 8 GPUs of one node with
+ * RCCL all-gather of C over xGMI only for the whole-node number".
+ *
+ * Why this shards with no exchange: Cx is per row of A and Cw depends only on B, so rank r computes
+ * the rows [m0, m0 + rows) of C from its rows of A and the replicated B -- bit-identical to the
+ * one-GPU call (op_mm.cuh:67-101 has no cross-row state).  The all-gather exists only to assemble
+ * the whole C on every GPU.
+ *
+ * Built as its own library (libqgemm_dist.so, links librccl) so libqgemm.so does not depend on
+ * RCCL.  Same conventions as qgemm.h: device pointers, 0 or a hipError_t / ncclResult_t code
+ * (ncclResult_t codes are returned as 1000 + code), work enqueued on `stream` (a hipStream_t).
+ */
+#ifndef QGEMM_DIST_H_
+#define QGEMM_DIST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "qgemm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QGEMM_COMM_ID_BYTES 128 /* = NCCL_UNIQUE_ID_BYTES (rccl.h:40) */
+
+/* Balanced contiguous row shards: rank r owns rows [*m0, *m0 + *rows) of an m-row matrix split over
+ * `world` ranks (the first m % world ranks get one row more).  Pure host arithmetic. */
+QGEMM_API int qgemm_shard_rows(int m, int world, int rank, int *m0, int *rows);
+
+/* This rank's share of op_mm_quantize(A, B, C, m, n, k): A and C are the FULL m-row matrices (row-major,
+ * leading dimensions k and n) as every rank sees them; only rows [m0, m0+rows) of A are read and of C
+ * written (pointer offsets A + m0*k, C + m0*n).  B (k x n) is replicated.  Bit-identical to those rows
+ * of the one-GPU call. */
+QGEMM_API int op_mm_quantize_shard(const float *A, const float *B, float *C, int m, int n, int k, int world,
+                                   int rank, void *stream);
+
+/* Communicators.  One process per GPU: rank 0 calls qgemm_comm_unique_id, shares the 128 bytes with the
+ * other ranks (any host channel), every rank calls qgemm_comm_init_rank on its own device.  One process
+ * driving ndev GPUs (the harness's -g): qgemm_comm_init_all fills comms[0..ndev). */
+QGEMM_API int qgemm_comm_unique_id(void *id_out /* QGEMM_COMM_ID_BYTES */);
+QGEMM_API int qgemm_comm_init_rank(void **comm, int world, const void *id, int rank);
+QGEMM_API int qgemm_comm_init_all(void **comms, int ndev, const int *devices);
+QGEMM_API int qgemm_comm_destroy(void *comm);
+
+/* In-place all-gather of C's row shards over RCCL: on entry rank r holds rows
+ * qgemm_shard_rows(m, world, r) of C (m x n row-major fp32, leading dimension n); on completion every
+ * rank holds all m rows.  m % world == 0: one ncclAllGather (send buffer = C + m0*n inside the receive
+ * buffer); otherwise one ncclBroadcast per owner inside a group.  Enqueued on `stream`. */
+QGEMM_API int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, void *comm, void *stream);
+
+/* One process, ndev GPUs (the harness's -g): the whole-node C4 step.  mode 0: every device's shard
+ * (op_mm_quantize_shard on devices[r] with A[r], B[r], C[r], streams[r]); mode 1: the shards, then the
+ * all-gather of C over comms[r]; mode 2: the all-gather alone (timed separately by the harness). */
+QGEMM_API int qgemm_node_mm_quantize(const float *const *A, const float *const *B, float *const *C, int m, int n,
+                                     int k, int ndev, const int *devices, void *const *comms,
+                                     void *const *streams, int mode);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QGEMM_DIST_H_ */

@@ -29,6 +29,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "build", "libqgemm.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "qgemm.h")
+DIST_LIB_PATH = os.path.join(PKG_DIR, "build", "libqgemm_dist.so")
+DIST_HEADER_PATH = os.path.join(REPO_DIR, "include", "qgemm_dist.h")
 
 DEFAULT_RANGE = 127.0  # `range` at every reference call site (test_quantize.cu:76, timing_quantize.cu:43)
 ROW_PAD = 256          # packed operand rows are padded to the GEMM macro-tile
@@ -63,10 +65,24 @@ EXPORTED_SYMBOLS = (
     "qgemm_version",
 )
 
+# Every symbol include/qgemm_dist.h declares (libqgemm_dist.so: M-shards + RCCL all-gather).
+DIST_EXPORTED_SYMBOLS = (
+    "qgemm_shard_rows",
+    "op_mm_quantize_shard",
+    "qgemm_comm_unique_id",
+    "qgemm_comm_init_rank",
+    "qgemm_comm_init_all",
+    "qgemm_comm_destroy",
+    "qgemm_allgather_rows",
+    "qgemm_node_mm_quantize",
+)
+COMM_ID_BYTES = 128
+
 HIP_ERROR_INVALID_VALUE = 1
 
 _lock = threading.Lock()
 _lib = None
+_dist = None
 
 
 class QGemmError(RuntimeError):
@@ -147,6 +163,87 @@ def load() -> ctypes.CDLL:
         L.qgemm_version.restype = ctypes.c_char_p
         _lib = L
         return L
+
+
+def load_dist() -> ctypes.CDLL:
+    """Load libqgemm_dist.so (M-sharded calls + the RCCL all-gather; no fallback)."""
+    global _dist
+    load()
+    with _lock:
+        if _dist is not None:
+            return _dist
+        if not os.path.exists(DIST_LIB_PATH):
+            raise RuntimeError(f"qgemm multi-GPU library not built: {DIST_LIB_PATH} missing (run build())")
+        D = ctypes.CDLL(DIST_LIB_PATH)
+        i32, vp = ctypes.c_int, ctypes.c_void_p
+        D.qgemm_shard_rows.argtypes = [i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        D.qgemm_shard_rows.restype = i32
+        D.op_mm_quantize_shard.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp]
+        D.op_mm_quantize_shard.restype = i32
+        D.qgemm_comm_unique_id.argtypes = [vp]
+        D.qgemm_comm_unique_id.restype = i32
+        D.qgemm_comm_init_rank.argtypes = [ctypes.POINTER(vp), i32, vp, i32]
+        D.qgemm_comm_init_rank.restype = i32
+        D.qgemm_comm_init_all.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(i32)]
+        D.qgemm_comm_init_all.restype = i32
+        D.qgemm_comm_destroy.argtypes = [vp]
+        D.qgemm_comm_destroy.restype = i32
+        D.qgemm_allgather_rows.argtypes = [vp, i32, i32, i32, i32, vp, vp]
+        D.qgemm_allgather_rows.restype = i32
+        D.qgemm_node_mm_quantize.argtypes = [vp, vp, vp, i32, i32, i32, i32, ctypes.POINTER(i32), vp, vp, i32]
+        D.qgemm_node_mm_quantize.restype = i32
+        _dist = D
+        return D
+
+
+def shard_rows(m: int, world: int, rank: int) -> tuple:
+    """(m0, rows) of rank's contiguous row shard (qgemm_shard_rows)."""
+    m0, rows = ctypes.c_int(), ctypes.c_int()
+    _check("qgemm_shard_rows", load_dist().qgemm_shard_rows(m, world, rank, ctypes.byref(m0), ctypes.byref(rows)))
+    return m0.value, rows.value
+
+
+def op_mm_quantize_shard(A, B, C, world: int, rank: int) -> None:
+    """Rows [m0, m0 + rows) of C = op_mm_quantize(A, B) on this rank (per-rank pointer offsets into the
+    full row-major A and C; bit-identical to those rows of the one-GPU call)."""
+    for t, nm in ((A, "A"), (B, "B"), (C, "C")):
+        _require_device_f32(t, nm)
+        assert t.is_contiguous(), f"{nm} must be contiguous row-major"
+    M, K = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == K and C.shape == (M, N), "A m x k, B k x n, C m x n"
+    _check("op_mm_quantize_shard", load_dist().op_mm_quantize_shard(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K,
+                                                                    world, rank, _stream(A.device)))
+
+
+class Comm:
+    """An RCCL communicator of libqgemm_dist.so (one rank per process, or world == 1 alone)."""
+
+    def __init__(self, world: int, rank: int, unique_id: bytes):
+        assert len(unique_id) == COMM_ID_BYTES
+        self.world, self.rank = world, rank
+        self._id = ctypes.create_string_buffer(unique_id, COMM_ID_BYTES)
+        self.handle = ctypes.c_void_p()
+        _check("qgemm_comm_init_rank",
+               load_dist().qgemm_comm_init_rank(ctypes.byref(self.handle), world, self._id, rank))
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        _check("qgemm_comm_unique_id", load_dist().qgemm_comm_unique_id(buf))
+        return buf.raw
+
+    def allgather_rows(self, C) -> None:
+        """In place: every rank's row shard of the full C (m x n) to every rank (qgemm_allgather_rows)."""
+        _require_device_f32(C, "C")
+        assert C.is_contiguous()
+        _check("qgemm_allgather_rows", load_dist().qgemm_allgather_rows(C.data_ptr(), C.shape[0], C.shape[1], self.world,
+                                                                        self.rank, self.handle, _stream(C.device)))
+
+    def close(self) -> None:
+        if self.handle:
+            _check("qgemm_comm_destroy", load_dist().qgemm_comm_destroy(self.handle))
+            self.handle = ctypes.c_void_p()
 
 
 def version() -> str:

@@ -1,0 +1,114 @@
+// dist.cpp -- libqgemm_dist.so: M-sharded op_mm_quantize + RCCL all-gather of C over xGMI
+// (include/qgemm_dist.h; SURVEY.md s8(b) multi-GPU driver, s8(e) partitioning and collective).
+//
+// No data-path collective in the compute: every rank packs its own rows of A and the replicated B and
+// runs the int8 GEMM on them (Cx is per row, Cw depends on B only), so a shard is bit-identical to the
+// same rows of the one-GPU call.  The all-gather only assembles the whole-node C.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include "../../include/qgemm_dist.h"
+
+namespace {
+
+int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? 0 : 1000 + (int)r; }
+
+}  // namespace
+
+extern "C" {
+
+int qgemm_shard_rows(int m, int world, int rank, int *m0, int *rows) {
+    if (m < 0 || world < 1 || rank < 0 || rank >= world || !m0 || !rows) return (int)hipErrorInvalidValue;
+    const int q = m / world, r = m % world;
+    *m0 = rank * q + (rank < r ? rank : r);
+    *rows = q + (rank < r ? 1 : 0);
+    return 0;
+}
+
+int op_mm_quantize_shard(const float *A, const float *B, float *C, int m, int n, int k, int world, int rank,
+                         void *stream) {
+    int m0 = 0, rows = 0;
+    const int e = qgemm_shard_rows(m, world, rank, &m0, &rows);
+    if (e) return e;
+    if (!A || !B || !C || n < 0 || k < 1) return (int)hipErrorInvalidValue;
+    if (rows == 0) return 0;
+    // per-rank pointer offsets: A + m0*k, C + m0*n
+    return op_mm_quantize_ex(A + (int64_t)m0 * k, k, 1, B, n, 1, C + (int64_t)m0 * n, n, 1, rows, n, k, 127.0f,
+                             stream);
+}
+
+int qgemm_comm_unique_id(void *id_out) {
+    if (!id_out) return (int)hipErrorInvalidValue;
+    return nccl_rc(ncclGetUniqueId(static_cast<ncclUniqueId *>(id_out)));
+}
+
+int qgemm_comm_init_rank(void **comm, int world, const void *id, int rank) {
+    if (!comm || !id || world < 1 || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
+    ncclUniqueId uid;
+    __builtin_memcpy(&uid, id, sizeof(uid));
+    ncclComm_t c = nullptr;
+    const int rc = nccl_rc(ncclCommInitRank(&c, world, uid, rank));
+    *comm = c;
+    return rc;
+}
+
+int qgemm_comm_init_all(void **comms, int ndev, const int *devices) {
+    if (!comms || ndev < 1) return (int)hipErrorInvalidValue;
+    return nccl_rc(ncclCommInitAll(reinterpret_cast<ncclComm_t *>(comms), ndev, devices));
+}
+
+int qgemm_comm_destroy(void *comm) {
+    if (!comm) return 0;
+    return nccl_rc(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
+}
+
+int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, void *comm, void *stream) {
+    if (!C || !comm || m < 0 || n < 0 || world < 1 || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (world == 1 || m == 0 || n == 0) return 0;
+    if (m % world == 0) {
+        // in place: rank r's send buffer is its own rows inside the receive buffer (recv + r*count)
+        const size_t count = (size_t)(m / world) * n;
+        return nccl_rc(ncclAllGather(C + (size_t)rank * count, C, count, ncclFloat32, c, s));
+    }
+    // unequal shards: each owner broadcasts its rows in place
+    ncclResult_t r = ncclGroupStart();
+    for (int root = 0; root < world && r == ncclSuccess; ++root) {
+        int m0 = 0, rows = 0;
+        qgemm_shard_rows(m, world, root, &m0, &rows);
+        if (rows == 0) continue;
+        float *p = C + (size_t)m0 * n;
+        r = ncclBroadcast(p, p, (size_t)rows * n, ncclFloat32, root, c, s);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    return nccl_rc(r != ncclSuccess ? r : r2);
+}
+
+int qgemm_node_mm_quantize(const float *const *A, const float *const *B, float *const *C, int m, int n, int k,
+                           int ndev, const int *devices, void *const *comms, void *const *streams, int mode) {
+    if (!A || !B || !C || !devices || !streams || ndev < 1 || mode < 0 || mode > 2 || (mode && !comms))
+        return (int)hipErrorInvalidValue;
+    int prev = 0;
+    hipError_t he = hipGetDevice(&prev);
+    if (he != hipSuccess) return (int)he;
+    int rc = 0;
+    for (int r = 0; r < ndev && rc == 0 && mode != 2; ++r) {
+        if ((he = hipSetDevice(devices[r])) != hipSuccess) rc = (int)he;
+        else rc = op_mm_quantize_shard(A[r], B[r], C[r], m, n, k, ndev, r, streams[r]);
+    }
+    if (rc == 0 && mode != 0 && ndev > 1) {
+        // one process drives every rank: the per-rank collectives go in one group
+        ncclResult_t g = ncclGroupStart();
+        for (int r = 0; r < ndev && rc == 0 && g == ncclSuccess; ++r) {
+            if ((he = hipSetDevice(devices[r])) != hipSuccess) rc = (int)he;
+            else rc = qgemm_allgather_rows(C[r], m, n, ndev, r, comms[r], streams[r]);
+        }
+        const ncclResult_t g2 = ncclGroupEnd();
+        if (rc == 0) rc = nccl_rc(g != ncclSuccess ? g : g2);
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+}  // extern "C"

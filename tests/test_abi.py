@@ -101,3 +101,40 @@ def test_reference_side_ctypes_binding_matches(qg):
     f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3
     f.restype = ctypes.c_int
     assert f(None, None, None, 1, 1, 1) == 1
+
+
+DIST_HEADER = os.path.join(REPO, "include", "qgemm_dist.h")
+
+
+def test_dist_library_exports_every_declared_symbol(qg):
+    text = open(DIST_HEADER).read()
+    fns = sorted(re.findall(r"^QGEMM_API\s+[\w\s\*]+?\b((?:op_|qgemm_)\w+)\s*\(", text, flags=re.M))
+    assert fns == sorted(qg.DIST_EXPORTED_SYMBOLS)
+    assert exported(qg.DIST_LIB_PATH) == fns, "libqgemm_dist.so exports must be exactly qgemm_dist.h"
+    # the RCCL call sites are real (rccl.h), not a shim
+    out = subprocess.run(["nm", "-D", "--undefined-only", qg.DIST_LIB_PATH], check=True, capture_output=True,
+                         text=True).stdout
+    for sym in ("ncclAllGather", "ncclBroadcast", "ncclCommInitRank", "ncclCommInitAll", "ncclGetUniqueId"):
+        assert sym in out, sym
+
+
+def test_shard_rows_partition_without_gpu(qg):
+    """qgemm_shard_rows: contiguous, balanced (sizes differ by <= 1), covering, = shard.row_range."""
+    import importlib
+    shard = importlib.import_module("qgemm_amd.shard")
+    for m in (0, 1, 7, 255, 4096, 65536, 65537):
+        for world in (1, 2, 3, 4, 8):
+            nxt = 0
+            for r in range(world):
+                m0, rows = qg.shard_rows(m, world, r)
+                assert m0 == nxt and rows >= 0
+                assert (m0, m0 + rows) == shard.row_range(m, world, r)
+                nxt = m0 + rows
+            assert nxt == m
+    D = qg.load_dist()
+    a, b = ctypes.c_int(), ctypes.c_int()
+    assert D.qgemm_shard_rows(8, 2, 2, ctypes.byref(a), ctypes.byref(b)) == 1  # rank >= world
+    assert D.qgemm_shard_rows(8, 0, 0, ctypes.byref(a), ctypes.byref(b)) == 1
+    # argument checks before any device work
+    assert D.op_mm_quantize_shard(None, None, None, 8, 8, 8, 2, 0, None) == 1
+    assert D.qgemm_allgather_rows(None, 8, 8, 2, 0, None, None) == 1

@@ -1,0 +1,71 @@
+"""Multi-GPU layer on one MI355X: the M-shard entry point (per-rank pointer offsets, bit-identical
+to the one-GPU call), the RCCL communicator + all-gather C-ABI (libqgemm_dist.so), and the C++
+multi-GPU driver (timing_quantize -g).  The 8-GPU run itself is the driver's scaling bench."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from util import assert_bits_equal
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(REPO, "quantized-gemm-for-transformer-inference_amd", "build")
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shards_assemble_the_one_gpu_result(qg, oracle, device, world):
+    M, N, K = 1000, 300, 520
+    X, W = oracle.inputs(M, N, K, 77)
+    Xd, Wd = torch.from_numpy(X).to(device), torch.from_numpy(W).to(device)
+    C = torch.full((M, N), float("nan"), device=device)
+    for r in range(world):  # each rank's call in turn, into its rows of the one full C
+        qg.op_mm_quantize_shard(Xd, Wd, C, world, r)
+    torch.cuda.synchronize()
+    assert_bits_equal(C.cpu().numpy(), oracle.quantized_mm(X, W), f"{world} shards")
+
+
+def test_rccl_comm_and_allgather_one_rank(qg, device):
+    comm = qg.Comm(1, 0, qg.Comm.unique_id())
+    try:
+        C = torch.arange(64 * 48, dtype=torch.float32, device=device).reshape(64, 48)
+        before = C.clone()
+        comm.allgather_rows(C)  # world 1: every row is already local
+        torch.cuda.synchronize()
+        assert torch.equal(C, before)
+    finally:
+        comm.close()
+
+
+def test_cpp_multi_gpu_driver_one_gpu():
+    """timing_quantize -g: shard compute + RCCL all-gather timed, every C bit-equal to one-GPU."""
+    out = subprocess.run([os.path.join(BUILD, "timing_quantize"), "-m", "1024", "-n", "768", "-k", "512", "-r", "3",
+                          "-g", "1"], check=True, capture_output=True, text=True, timeout=120).stdout
+    node = json.loads(out.strip().splitlines()[-1])["node"]
+    assert node["gpus"] == 1 and node["bit_identical_to_one_gpu"] is True and node["mismatches"] == 0
+    assert node["compute_ms"] > 0 and node["sharded_gemms_per_s"] > 0
+
+
+def test_timing_quantize_prints_the_reference_lines():
+    """The reference harness's output format (timing_quantize.cu:33-34,63-64,69-70,108,112-113) at its
+    own shape 2048x512x512 (the stashed side of timing_quantize.cu:77-79)."""
+    r = 2
+    out = subprocess.run([os.path.join(BUILD, "timing_quantize"), "-m", "2048", "-n", "512", "-k", "512", "-r", str(r)],
+                         check=True, capture_output=True, text=True, timeout=120).stdout.splitlines()
+    i = 0
+    for it in range(r):
+        assert out[i] == "Time taken for matmul: " and float(out[i + 1]) > 0
+        assert out[i + 2] == "Time taken for quantized matmul: " and float(out[i + 3]) > 0
+        assert out[i + 4] == "Mean Quantization error: " and abs(float(out[i + 5])) < 1e-2
+        t, qt = (float(x) for x in out[i + 6].split())
+        assert t == float(out[i + 1]) and qt == float(out[i + 3])
+        i += 7
+    assert out[i] == "Final times"
+    avg = [float(x) for x in out[i + 1].split()]
+    assert len(avg) == 2 and all(a > 0 for a in avg)
+    js = json.loads(out[i + 2])
+    assert js["m"] == 2048 and js["quantized_gemms_per_s"] > 0

@@ -194,19 +194,27 @@ def test_device_generator_matches_oracle(qg, oracle, device):
     assert_bits_equal(t.cpu().numpy(), oracle.uniform((1 << 20,), seed=9), "fill_uniform")
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (2048, 16384, 4096), (2048, 4096, 16384)])
-def test_full_size_sampled_rows(qg, oracle, device, M, N, K):
-    """BASELINE configs 2 and 3 at full size: inputs generated on the GPU (bit-identical to the
-    oracle's generator), output rows sampled across every macro-tile row and checked bit-exactly."""
+# BASELINE configs at full size: C2 4096^3 (one 256x256 tile per CU), C3 FFN up / down (down: K > 4096,
+# the two-pass pack and split-K), the C4 shard 8192 x 4096 x 4096 (two tiles per CU) -- every output bit.
+@pytest.mark.parametrize("M,N,K,cfg", [(4096, 4096, 4096, "c2"), (2048, 16384, 4096, "c3_up"),
+                                       (2048, 4096, 16384, "c3_down"), (8192, 4096, 4096, "c4_shard")])
+def test_full_size_every_output(qg, oracle, device, M, N, K, cfg):
+    """Inputs generated on the GPU (bit-identical to the oracle's generator); the WHOLE output compared
+    bit for bit with the oracle's chain on the same inputs.  C2 goes through the flat north-star entry
+    point op_mm_quantize(A, B, C, M, N, K) on the null stream, the others through the Python mirror."""
     X = qg.fill_uniform(torch.empty((M, K), device=device), seed=2 * 31)
     W = qg.fill_uniform(torch.empty((K, N), device=device), seed=2 * 31 + 1)
-    O = qg.op_mm_quantize(X, W)
+    if cfg == "c2":
+        O = torch.full((M, N), float("nan"), device=device)
+        torch.cuda.synchronize()
+        assert qg.load().op_mm_quantize(X.data_ptr(), W.data_ptr(), O.data_ptr(), M, N, K) == 0
+    else:
+        O = qg.op_mm_quantize(X, W)
     torch.cuda.synchronize()
     Xh, Wh = oracle.uniform((M, K), 2 * 31), oracle.uniform((K, N), 2 * 31 + 1)
-    assert_bits_equal(X.cpu().numpy()[:3], Xh[:3], "X generation")
-    rows = np.unique(np.concatenate([np.arange(0, M, 257), [M - 1, 255, 256, M // 2]])).astype(np.int32)
-    want = oracle.quantized_mm_rows(Xh, Wh, rows)
-    assert_bits_equal(O[torch.from_numpy(rows).long().to(device)].cpu().numpy(), want, f"{M}x{N}x{K} rows")
+    assert_bits_equal(X.cpu().numpy(), Xh, "X generation")
+    assert_bits_equal(W.cpu().numpy(), Wh, "W generation")
+    assert_bits_equal(O.cpu().numpy(), oracle.quantized_mm(Xh, Wh), f"{cfg} {M}x{N}x{K} full output")
 
 
 def test_strided_views(qg, oracle, device):
