@@ -291,7 +291,7 @@ __device__ __forceinline__ float epi_extra(float o, const float *sB, int jl) {
     return o;
 }
 
-template <int kMode, int kEpi = kEpiNone>
+template <int kMode, int kEpi = kEpiNone, bool kNt = false>
 __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (&acc)[8][4], int tm, int tn, int wm,
                                            int wn, int lane, int tid) {
     const int gi0 = tm * BM, gj0 = tn * BN;
@@ -365,7 +365,13 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
                 const float4 v = *reinterpret_cast<const float4 *>(T + rr * BN + c4);
                 const int j = gj0 + c4;
                 if (full) {
-                    *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = v;
+                    if constexpr (kNt) {
+                        typedef float v4f __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w},
+                                                    reinterpret_cast<v4f *>(C + (int64_t)i * p.csh + j));
+                    } else {
+                        *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = v;
+                    }
                 } else {
                     const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
 // into a slot comes after the barrier that follows the last reads of it (lgkmcnt(0) before each
 // R-slot barrier).  Barrier counts match: lead 1 + 2nk, lag 2 + 2nk - 1.
 // lab-only flags (kPP*): in-kernel stamps, ablations
-enum PPFlags { kPPStamp = 1, kPPNoDma = 2, kPPNoStore = 4 };
+enum PPFlags { kPPStamp = 1, kPPNoDma = 2, kPPNoStore = 4, kPPNtStore = 8 };
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_pp_stamp[4096 * 6];
 #endif
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
             }
     };
 #else
-    static_assert(kFlags == 0, "lab flags need QGEMM_LAB");
+    static_assert((kFlags & ~kPPNtStore) == 0, "lab flags need QGEMM_LAB");
     auto stamp = [](int) {};
 #endif
     stamp(0);
@@ -713,7 +719,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
     if (S > 1 && !splitk_combine<8, 4, 8>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice, S, wave,
                                           lane, tid))
         return;
-    epilogue16<(kFlags & kPPNoStore) ? kStoreNone : kStoreLds, kEpi>(p, lds, acc, tm, tn, wm, wn, lane, tid);
+    epilogue16<(kFlags & kPPNoStore) ? kStoreNone : kStoreLds, kEpi, (kFlags & kPPNtStore) != 0>(p, lds, acc, tm, tn, wm,
+                                                                                                 wn, lane, tid);
     stamp(2);
 }
 

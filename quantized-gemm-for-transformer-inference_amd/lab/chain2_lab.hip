@@ -10,6 +10,7 @@
 #include <cstring>
 #include <hip/hip_ext.h>
 
+#define QGEMM_LAB 1
 #include "../csrc/pack.hip"
 #include "../csrc/gemm_i8_kernels.h"
 
@@ -78,16 +79,34 @@ int main(int argc, char **argv) {
             auto med = [](std::vector<float> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.f : v[v.size() / 2]; };
             printf("%-30s gemm %7.2f us  pack %7.2f us  whole %7.2f us\n", names[mode], med(tg), med(tp), med(tw));
         }
-    // back-to-back chain throughput (as bench.py): pack, gemm, pack, gemm ...
-    for (int round = 0; round < 3; ++round) {
-        CK(hipEventRecord(e[6]));
-        for (int i = 0; i < 200; ++i) {
-            CK(launch_pack_single_pass(X, K, M, K, va, W, N, N, vb, 127.f, 0));
-            gemm_i8_pp<1, kEpiNone><<<grid, kThreads>>>(p);
+    // back-to-back chain throughput (as bench.py): pack, gemm, pack, gemm ... -- plain vs nt (non-temporal)
+    // output stores: does keeping C out of the Infinity Cache leave X and W resident for the next pack?
+    for (int round = 0; round < 3; ++round)
+        for (int nt = 0; nt < 2; ++nt) {
+            CK(hipEventRecord(e[6]));
+            for (int i = 0; i < 200; ++i) {
+                CK(launch_pack_single_pass(X, K, M, K, va, W, N, N, vb, 127.f, 0));
+                if (nt) gemm_i8_pp<1, kEpiNone, kPPNtStore><<<grid, kThreads>>>(p);
+                else gemm_i8_pp<1, kEpiNone><<<grid, kThreads>>>(p);
+            }
+            CK(hipEventRecord(e[7])); CK(hipEventSynchronize(e[7]));
+            float ms; CK(hipEventElapsedTime(&ms, e[6], e[7]));
+            printf("chain back to back (%s C stores): %.2f us per call\n", nt ? "nt" : "plain", ms * 1000 / 200);
         }
-        CK(hipEventRecord(e[7])); CK(hipEventSynchronize(e[7]));
-        float ms; CK(hipEventElapsedTime(&ms, e[6], e[7]));
-        printf("chain back to back: %.2f us per call\n", ms * 1000 / 200);
+    // per-kernel times inside the chain, nt vs plain
+    for (int nt = 0; nt < 2; ++nt) {
+        std::vector<float> tg, tp;
+        for (int i = 0; i < 40; ++i) {
+            pack(e[0], e[1]);
+            if (nt) hipExtLaunchKernelGGL((gemm_i8_pp<1, kEpiNone, kPPNtStore>), grid, dim3(kThreads), 0, 0, e[2], e[3], 0, p);
+            else gemm(e[2], e[3]);
+            CK(hipEventSynchronize(e[3]));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e[2], e[3])); tg.push_back(ms * 1000);
+            CK(hipEventElapsedTime(&ms, e[0], e[1])); tp.push_back(ms * 1000);
+        }
+        std::sort(tg.begin(), tg.end()); std::sort(tp.begin(), tp.end());
+        printf("%s C stores: pack %.2f us, gemm %.2f us (medians)\n", nt ? "nt" : "plain", tp[tp.size() / 2], tg[tg.size() / 2]);
     }
     return 0;
 }
