@@ -125,6 +125,16 @@ def load_pkg():
     return qg
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(M, N, K, target_s):
     """Time the oracle's quantized chain (and the unquantized fp32 GEMM) on the host cores.
 
@@ -149,6 +159,8 @@ def cpu_baseline(M, N, K, target_s):
         "value": reps / tq,
         "unit": "GEMMs/s",
         "cores": threads,
+        "cpu_model": cpu_model(),
+        "host_cpus_visible": os.cpu_count(),
         "kind": "port",
         "sample": f"oracle/ C restatement of the reference chain (op_mm.cuh:67-101), full {M}x{N}x{K} "
                   f"problem x{reps} = {tq:.1f} s on {threads} OpenMP threads; unquantized fp32 op_mm "
