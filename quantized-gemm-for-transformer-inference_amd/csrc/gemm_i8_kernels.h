@@ -542,8 +542,14 @@ enum PPFlags { kPPStamp = 1, kPPNoDma = 2, kPPNoStore = 4, kPPNtStore = 8 };
 __device__ unsigned long long g_pp_stamp[4096 * 6];
 #endif
 
+// LDS bytes of the ping-pong body (staging ring + scales/bias/flag)
+template <int kEpi>
+constexpr int pp_lds_bytes() { return kLdsBytes + (kEpi >= kEpiBias ? 3072 : 2048); }
+
+// One 256 x 256 tile (k-slice `slice` of S) of the ping-pong GEMM on a 512-thread block; `lds` holds
+// pp_lds_bytes<kEpi>() bytes.  The body of gemm_i8_pp and of the fused pack+GEMM launch.
 template <int kDma, int kEpi = kEpiNone, int kFlags = 0>
-__global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
+__device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int tile, int slice, int S) {
 #ifdef QGEMM_LAB
     auto stamp = [&](int i) __attribute__((always_inline)) {
         if constexpr (kFlags & kPPStamp)
@@ -557,14 +563,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
     auto stamp = [](int) {};
 #endif
     stamp(0);
-    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + (kEpi >= kEpiBias ? 3072 : 2048)];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const bool lead = wm == 0;
-    const int S = p.splits > 1 ? p.splits : 1;
-    const int wid = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile = wid / S, slice = wid - tile * S;
     int tm, tn;
     group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
     const int nk_all = (int)(p.k_pad / BK);
@@ -722,6 +724,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
     epilogue16<(kFlags & kPPNoStore) ? kStoreNone : kStoreLds, kEpi, (kFlags & kPPNtStore) != 0>(p, lds, acc, tm, tn, wm,
                                                                                                  wn, lane, tid);
     stamp(2);
+}
+
+template <int kDma, int kEpi = kEpiNone, int kFlags = 0>
+__global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[pp_lds_bytes<kEpi>()];
+    const int S = p.splits > 1 ? p.splits : 1;
+    const int wid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = wid / S;
+    pp_tile_body<kDma, kEpi, kFlags>(p, lds, tile, wid - tile * S, S);
 }
 
 // ------------------------------------------------------------------------------------------------
