@@ -856,8 +856,14 @@ __global__ __launch_bounds__((SmallTile<TB, kDepth>::kThreads), (SmallTile<TB, k
 #pragma unroll
         for (int s = 0; s < kDepth - 1; ++s) stage(min(kt0 + s, last), s);
         for (int kt = 0; kt < nk; ++kt) {
+            // stage kt landed for this wave's pieces; a RAW barrier then makes it visible to every wave (and
+            // every wave is done reading stage kt - 1's slot, which the DMA below refills).  Not
+            // __syncthreads(): with LDS-DMA in flight its fence emits vmcnt(0), which drained the whole
+            // ring every k-step (one stage in flight whatever kDepth was).
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDepth - 2) * T_::kLoadsPerStage) : "memory");
-            __syncthreads();  // stage kt visible to every wave; every wave is done with stage kt - 1's slot
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
             stage(min(kt0 + kt + kDepth - 1, last), (kt + kDepth - 1) % kDepth);
             const int cur = kt % kDepth;
             read_frags(a0, b0, cur, 0);
