@@ -246,12 +246,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void mm_f32_dma_kernel(
                     : *reinterpret_cast<const float *>(st_ + A_BYTES + b_rd[b] + s * 4 * TN * 4);                    \
         }                                                                                                            \
     } while (0)
-    // wait until tile KT's DMA landed with up to LEFT younger tiles still in flight, in every wave
+    // wait until tile KT's DMA landed with up to LEFT younger tiles still in flight, in every wave: this
+    // wave's counted vmcnt, then a RAW barrier (__syncthreads()' fence would wait vmcnt(0) while LDS-DMA
+    // is in flight, i.e. drain the whole ring every k tile)
 #define QG_LANDED(LEFT)                                                                                              \
     do {                                                                                                             \
         __builtin_amdgcn_s_waitcnt(vmcnt_imm((LEFT) * IPW));                                                         \
-        if (NW > 1) __syncthreads();                                                                                 \
-        else __builtin_amdgcn_sched_barrier(0);                                                                      \
+        if (NW > 1) {                                                                                                \
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
+            __builtin_amdgcn_s_barrier();                                                                            \
+            asm volatile("" ::: "memory");                                                                           \
+        } else {                                                                                                     \
+            __builtin_amdgcn_sched_barrier(0);                                                                       \
+        }                                                                                                            \
     } while (0)
 #define QG_STEP(KT, CUR, NXT)                                                                                        \
     do {                                                                                                             \
