@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 import _pkg  # noqa: E402
 
-qg = _pkg.package()
+qg = _pkg.package(build=False)
 seq, d, H, dff, blocks = 512, 1024, 16, 4096, 2
 dev = torch.device("cuda", 0)
 enc = qg.Encoder(d, H, dff, blocks, max_seq=seq, seed=1)
