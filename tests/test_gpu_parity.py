@@ -394,3 +394,28 @@ def test_concurrent_streams_with_own_workspaces(qg, oracle, device):
     torch.cuda.synchronize()
     for i, (_, _, want, _, O, _) in enumerate(cases):
         assert_bits_equal(O.cpu().numpy(), want, f"stream {i}")
+
+
+def test_lds_dma_rings_repeat_race_screen(qg, oracle, device):
+    """Race screen for the LDS-DMA rings that keep stages in flight across a raw s_barrier (the 3-stage
+    64-tile int8 ring, with and without split-K, and the fp32 DMA ring): many back-to-back calls of each,
+    every output bit compared -- an early read of a stage shows up as rare wrong tiles, not as a fault
+    (cdna_hip_programming.md s5 'Read a staged buffer one phase AFTER the wait that retires it')."""
+    for M, N, K, reps in [(512, 3072, 1024, 40), (512, 1024, 4096, 40), (130, 70, 640, 40)]:
+        X, W = oracle.inputs(M, N, K, 81)
+        want = oracle.quantized_mm(X, W)
+        pa, pb = qg.pack_a(_dev(X, device)), qg.pack_b(_dev(W, device))
+        outs = [torch.empty((M, N), device=device) for _ in range(reps)]
+        for O in outs:
+            qg.mm_packed(pa, pb, O)
+        torch.cuda.synchronize()
+        for i, O in enumerate(outs):
+            assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} repeat {i}")
+    M, N, K = 512, 512, 1024
+    X, W = oracle.inputs(M, N, K, 82)
+    want = oracle.mm_fp32(X, W)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    outs = [qg.mm_fp32(Xd, Wd) for _ in range(30)]
+    torch.cuda.synchronize()
+    for i, C in enumerate(outs):
+        assert_bits_equal(C.cpu().numpy(), want, f"fp32 {M}x{N}x{K} repeat {i}")
