@@ -309,6 +309,14 @@ int qgemm_mm_outlier(const float *A, const float *B, float *C, int m, int n, int
     hipStream_t s = static_cast<hipStream_t>(stream);
     char *scratch = static_cast<char *>(workspace);
     char *ws2 = scratch + align256(outlier_scratch_bytes(m, n, k));
+    {
+        // fast path: the packed operands in the plain chain's slots of ws2 (no split-K: no tickets)
+        char *pa = ws2 + align256(gemm_scratch_bytes(m, n, k));
+        char *pb = pa + align256(packed_bytes(m, k));
+        const hipError_t e = outlier_fast(A, B, C, m, n, k, threshold, scratch, packed_view(pa, m, k),
+                                          packed_view(pb, n, k), kDefaultRange, s);
+        if (e != hipErrorNotSupported) return err(e);
+    }
     float *Xm = nullptr, *Wm = nullptr;
     hipError_t e = outlier_prepare(A, k, B, n, m, n, k, threshold, scratch, &Xm, &Wm, s);
     if (e != hipSuccess) return err(e);

@@ -160,6 +160,21 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
     return relu ? launch_v3<kEpiBiasRelu>(p, grid, stream) : launch_v3<kEpiBias>(p, grid, stream);
 }
 
+bool gemm_outlier_ok(int m, int n, int k) {
+    const GemmPlan g = gemm_plan(m, n, k);
+    return g.tile == 256 && g.splits == 1;
+}
+
+hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b, float *C, int64_t csh, int m, int n,
+                                       float inv_r2, const float *xo, const float *wo, int64_t wo_ld, const int *ocount,
+                                       hipStream_t stream) {
+    if (!shape_ok(a, b) || !gemm_outlier_ok(m, n, (int)a.k_pad) || (wo_ld % BN) != 0) return hipErrorNotSupported;
+    const GemmPlan g = gemm_plan(m, n, (int)a.k_pad);
+    GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, 1, m, n, a.k_pad, g.tiles_m, g.tiles_n,
+               inv_r2, 1, nullptr, nullptr, nullptr, 0, xo, wo, ocount, wo_ld};
+    return launch_v3<kEpiOutlier>(p, dim3((unsigned)(g.tiles_m * g.tiles_n)), stream);
+}
+
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n, hipStream_t stream) {
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, Acc, n, 1, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),

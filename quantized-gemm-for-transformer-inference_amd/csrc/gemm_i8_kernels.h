@@ -73,11 +73,19 @@ struct GemmArgs {
     unsigned *tickets;  // tiles words, zeroed before every launch
     const float *bias;  // n floats, added after the dequantize (kEpi >= 1)
     int reset_tickets;  // the reducer re-zeroes its ticket (scratch zeroed once at allocation)
+    // kEpiOutlier: xo [m][cnt], wo [cnt][wo_ld] (16-B aligned rows), cnt = *ocount on the device
+    const float *xo;
+    const float *wo;
+    const int *ocount;
+    int64_t wo_ld;
 };
 
 // Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
 // y = fl(O + b[j]) then relu(y) = (y < 0 ? 0 : y) -- each its own rounding, as the separate launches.
-enum EpiMode { kEpiNone = 0, kEpiBias = 1, kEpiBiasRelu = 2 };
+// kEpiOutlier: the LLM.int8() decomposition's fp32 part, O = fl(O8 + fmaf chain over the outlier
+// columns in ascending k of xo[i][t] * wo[t][j]) (outlier.hip; the oracle's oracle_mm_outlier)
+enum EpiMode { kEpiNone = 0, kEpiBias = 1, kEpiBiasRelu = 2, kEpiOutlier = 3 };
+constexpr bool has_bias(int e) { return e == kEpiBias || e == kEpiBiasRelu; }
 
 constexpr int64_t kSlabInts = (int64_t)BM * BN;
 
@@ -286,9 +294,81 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v1(GemmArgs p) {
 //   kStoreNone   : ablation -- keep the accumulators live, store nothing.
 template <int kEpi>
 __device__ __forceinline__ float epi_extra(float o, const float *sB, int jl) {
-    if constexpr (kEpi >= kEpiBias) o = __fadd_rn(o, sB[jl]);
+    if constexpr (has_bias(kEpi)) o = __fadd_rn(o, sB[jl]);
     if constexpr (kEpi == kEpiBiasRelu) o = (o < 0.0f) ? 0.0f : o;
     return o;
+}
+
+// kEpiOutlier store of one 128-row half of the tile (rows i0 .. i0 + 127 in T): O = fl(O8 + fmaf chain
+// from +0 over the outlier columns in ascending k).  A wave owns rows i0 + w + 8q, a lane 4 columns; the
+// chain runs for 8 rows at once, 4 outlier columns per step: one load brings the 8 x 4 xo values (lane
+// 8g + tt: row g, column tt), v_readlane hands each to the wave as a scalar, one float4 of wo per column
+// serves the 8 rows.  Columns past n read wo's padding and are never stored.
+__device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const float *T, int i0, int gj0, int c4,
+                                                      int tid, bool full) {
+    const int ocnt = *p.ocount;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int j = gj0 + c4;
+    const float *wr = p.wo + j;
+    float *C = static_cast<float *>(p.C);
+#pragma unroll 1
+    for (int q0 = 0; q0 < 16; q0 += 8) {
+        const int ib = i0 + wv + 8 * q0;  // rows ib + 8g, g < 8
+        if (ib >= p.m) break;
+        const float *xl = p.xo + (int64_t)min(ib + 8 * (lane >> 3), p.m - 1) * ocnt + (lane & 7);
+        float c[8][4];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) c[g][0] = c[g][1] = c[g][2] = c[g][3] = 0.0f;
+        // 4 columns per step; step t0 + 4's loads are issued before step t0's arithmetic
+        auto load_step = [&](int t0, float &xv, float4 (&w4)[4]) {
+            const int tn = min(4, ocnt - t0);
+            xv = (lane & 7) < tn ? xl[t0] : 0.0f;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+                w4[tt] = tt < tn ? *reinterpret_cast<const float4 *>(wr + (int64_t)(t0 + tt) * p.wo_ld)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        };
+        float xn;
+        float4 wn[4];
+        load_step(0, xn, wn);
+#pragma unroll 1
+        for (int t0 = 0; t0 < ocnt; t0 += 4) {
+            const int tn = min(4, ocnt - t0);  // uniform
+            const float xv = xn;
+            float4 w4[4];
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) w4[tt] = wn[tt];
+            if (t0 + 4 < ocnt) load_step(t0 + 4, xn, wn);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                if (tt >= tn) break;
+#pragma unroll
+                for (int g = 0; g < 8; ++g) {
+                    const float xs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), 8 * g + tt));
+                    c[g][0] = __fmaf_rn(xs, w4[tt].x, c[g][0]);
+                    c[g][1] = __fmaf_rn(xs, w4[tt].y, c[g][1]);
+                    c[g][2] = __fmaf_rn(xs, w4[tt].z, c[g][2]);
+                    c[g][3] = __fmaf_rn(xs, w4[tt].w, c[g][3]);
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const int i = ib + 8 * g;
+            if (i >= p.m) break;
+            const float4 o = *reinterpret_cast<const float4 *>(T + (i - i0) * BN + c4);
+            const float vv[4] = {__fadd_rn(o.x, c[g][0]), __fadd_rn(o.y, c[g][1]), __fadd_rn(o.z, c[g][2]),
+                                 __fadd_rn(o.w, c[g][3])};
+            if (full) {
+                *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+            }
+        }
+    }
 }
 
 template <int kMode, int kEpi = kEpiNone, bool kNt = false>
@@ -314,7 +394,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
     __syncthreads();  // every wave is done with the staging ring
     if (tid < BM) sCx[tid] = p.Cx[gi0 + tid];
     else sCw[tid - BM] = p.Cw[gj0 + tid - BM];
-    if constexpr (kEpi >= kEpiBias)
+    if constexpr (has_bias(kEpi))
         if (tid < BN) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
     if constexpr (kMode == kStoreDirect) {
         __syncthreads();
@@ -358,6 +438,12 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
             }
             __syncthreads();
             const int c4 = (tid & 63) * 4;
+            if constexpr (kEpi == kEpiOutlier) {
+                if (*p.ocount > 0) {
+                    epilogue_outlier_half(p, T, gi0 + half * 128, gj0, c4, tid, full);
+                    continue;
+                }
+            }
 #pragma unroll 4
             for (int rr = tid >> 6; rr < 128; rr += kThreads / 64) {
                 const int i = gi0 + half * 128 + rr;
@@ -441,7 +527,7 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last
 template <int kMode, bool kDequant, int kFlags = 0, int kEpi = kEpiNone>
 __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
     // + scales (and bias) for the epilogue
-    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + (kEpi >= kEpiBias ? 3072 : 2048)];
+    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + (has_bias(kEpi) ? 3072 : 2048)];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -544,7 +630,7 @@ __device__ unsigned long long g_pp_stamp[4096 * 6];
 
 // LDS bytes of the ping-pong body (staging ring + scales/bias/flag)
 template <int kEpi>
-constexpr int pp_lds_bytes() { return kLdsBytes + (kEpi >= kEpiBias ? 3072 : 2048); }
+constexpr int pp_lds_bytes() { return kLdsBytes + (has_bias(kEpi) ? 3072 : 2048); }
 
 // One 256 x 256 tile (k-slice `slice` of S) of the ping-pong GEMM on a 512-thread block; `lds` holds
 // pp_lds_bytes<kEpi>() bytes.  The body of gemm_i8_pp and of the fused pack+GEMM launch.
@@ -887,7 +973,7 @@ __global__ __launch_bounds__((SmallTile<TB, kDepth>::kThreads), (SmallTile<TB, k
     __syncthreads();  // every wave is done with the staging ring
     if (tid < TB) sCx[tid] = p.Cx[gi0 + tid];
     else if (tid < 2 * TB) sCw[tid - TB] = p.Cw[gj0 + tid - TB];
-    if constexpr (kEpi >= kEpiBias)
+    if constexpr (has_bias(kEpi))
         if (tid < TB) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
     __syncthreads();
     float *T = reinterpret_cast<float *>(lds);  // [TB][TB] fp32 in the ring

@@ -7,6 +7,17 @@
 //   O8  = op_quantized_mm(X', W'), X' = X with the outlier columns zeroed, W' = W with those rows zeroed
 //   Co  = fmaf chain from +0 over the outlier columns in ascending k: X[i,k] * W[k,j]
 //   O   = fl(O8 + Co)            (no outlier columns: O = O8, the plain path)
+//
+// One call, fast path (row-major operands on the single-pass pack + 256-tile GEMM): four launches --
+//   outlier_flags  : X read once in full-row float4 loads; per 64-row chunk a bitmask of its outlier
+//                    columns (every word written: nothing to clear per call)
+//   outlier_index  : one block ORs the chunk masks into the column mask, the per-word ranks, the
+//                    ascending list of outlier columns and their count (stays on the device)
+//   the pack       : the single pass with the mask (pack.hip): X'/W' quantized without materialising
+//                    them, the outlier columns' values written compactly (xo [m][cnt], wo [cnt][n_pad])
+//   the GEMM       : the int8 part with the fp32 chain added in its store epilogue (gemm_i8_kernels.h)
+// Other shapes: flags + index, X'/W' materialised by a masking pass, the plain drop-in on them, and a
+// correction kernel adding the chain to O.
 #include <algorithm>
 
 #include "qgemm_internal.h"
@@ -15,63 +26,110 @@ namespace qgemm {
 
 namespace {
 
+constexpr int kChunkRows = 64;     // rows per flags block
+constexpr int kFlagCols = 1024;    // columns per flags block (256 threads x 4)
+
 // AbsCompareLTEConstFunc (op_elemwise.cuh:296-304): 0 when a in [-b, b], else 1 (NaN -> 1)
 __device__ __forceinline__ bool is_outlier(float a, float b) {
     return !(((a >= 0) & (a <= b)) | ((a <= 0) & (-a <= b)));
 }
 
-// flags[c] |= outlier over a chunk of rows; thread per column (coalesced along the row)
-__global__ __launch_bounds__(256) void outlier_cols_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
-                                                           float t, int rows_per_block,
-                                                           unsigned *__restrict__ flags) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= k) return;
-    const int r0 = blockIdx.y * rows_per_block, r1 = min(m, r0 + rows_per_block);
-    bool any = false;
-    for (int r = r0; r < r1; ++r) any |= is_outlier(X[(int64_t)r * xsh + c], t);
-    if (any) atomicOr(flags + c, 1u);
+// partial[chunk][word]: bit c of word w set when column 32w + c holds an outlier in rows
+// [64 chunk, 64 chunk + 64).  Thread t: columns 1024 bx + 4t .. +3.
+template <bool VEC>
+__global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
+                                                            float t, uint32_t *__restrict__ partial, int nwords) {
+    const int tid = threadIdx.x;
+    const int c = blockIdx.x * kFlagCols + 4 * tid;
+    const int r0 = blockIdx.y * kChunkRows, r1 = min(m, r0 + kChunkRows);
+    uint32_t nib = 0;
+    if (c < k) {
+        if constexpr (VEC) {
+            const float *p = X + (int64_t)r0 * xsh + c;
+#pragma unroll 16
+            for (int r = r0; r < r1; ++r, p += xsh) {
+                const float4 x = *reinterpret_cast<const float4 *>(p);
+                nib |= (is_outlier(x.x, t) ? 1u : 0u) | (is_outlier(x.y, t) ? 2u : 0u) | (is_outlier(x.z, t) ? 4u : 0u) |
+                       (is_outlier(x.w, t) ? 8u : 0u);
+            }
+        } else {
+            for (int r = r0; r < r1; ++r)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (c + e < k && is_outlier(X[(int64_t)r * xsh + c + e], t)) nib |= 1u << e;
+        }
+    }
+    // eight consecutive lanes hold one 32-column word
+    uint32_t word = nib << (4 * (tid & 7));
+    word |= __shfl_xor(word, 1, 64);
+    word |= __shfl_xor(word, 2, 64);
+    word |= __shfl_xor(word, 4, 64);
+    const int w = blockIdx.x * (kFlagCols / 32) + (tid >> 3);
+    if ((tid & 7) == 0 && w < nwords) partial[(int64_t)blockIdx.y * nwords + w] = word;
 }
 
-// ascending indices of the flagged columns (one block, chunked prefix sum); count at idx[-1] slot
-__global__ __launch_bounds__(1024) void outlier_index_kernel(const unsigned *__restrict__ flags, int k,
-                                                             int *__restrict__ idx, int *__restrict__ count) {
+// bits[w] = OR of the chunk masks, rank[w] = set bits below word w, idx[1 + ...] = the outlier columns in
+// ascending order, idx[0] = their count.  One block.
+__global__ __launch_bounds__(1024) void outlier_index_kernel(const uint32_t *__restrict__ partial, int nchunks,
+                                                             int nwords, uint32_t *__restrict__ bits,
+                                                             int *__restrict__ rank, int *__restrict__ idx) {
     __shared__ int scan[1024];
     __shared__ int base;
-    if (threadIdx.x == 0) base = 0;
+    const int tid = threadIdx.x;
+    if (tid == 0) base = 0;
     __syncthreads();
-    for (int c0 = 0; c0 < k; c0 += 1024) {
-        const int c = c0 + threadIdx.x;
-        const int f = (c < k && flags[c]) ? 1 : 0;
-        scan[threadIdx.x] = f;
+    for (int w0 = 0; w0 < nwords; w0 += 1024) {
+        const int w = w0 + tid;
+        uint32_t word = 0;
+        if (w < nwords) {
+            int ch = 0;
+            for (; ch + 16 <= nchunks; ch += 16) {  // 16 loads in flight
+                uint32_t u[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) u[e] = partial[(int64_t)(ch + e) * nwords + w];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) word |= u[e];
+            }
+            for (; ch < nchunks; ++ch) word |= partial[(int64_t)ch * nwords + w];
+        }
+        const int pc = __popc(word);
+        scan[tid] = pc;
         __syncthreads();
         for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-            const int v = threadIdx.x >= off ? scan[threadIdx.x - off] : 0;
+            const int v = tid >= off ? scan[tid - off] : 0;
             __syncthreads();
-            scan[threadIdx.x] += v;
+            scan[tid] += v;
             __syncthreads();
         }
-        if (f) idx[base + scan[threadIdx.x] - 1] = c;
+        const int below = base + scan[tid] - pc;
+        if (w < nwords) {
+            bits[w] = word;
+            rank[w] = below;
+            int j = 0;
+            for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
+        }
         __syncthreads();
-        if (threadIdx.x == 1023) base += scan[1023];
+        if (tid == 1023) base += scan[1023];
         __syncthreads();
     }
-    if (threadIdx.x == 0) *count = base;
+    if (tid == 0) idx[0] = base;
 }
 
-// X' (outlier columns zeroed) and W' (outlier rows zeroed), contiguous outputs
+__device__ __forceinline__ bool bit_of(const uint32_t *bits, int64_t c) { return (bits[c >> 5] >> (c & 31)) & 1u; }
+
+// X' (outlier columns zeroed) and W' (outlier rows zeroed), contiguous outputs; block = one row of X (the
+// first m blocks) or of W
 __global__ __launch_bounds__(256) void outlier_mask_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
                                                            const float *__restrict__ W, int64_t wsh, int n,
-                                                           const unsigned *__restrict__ flags,
-                                                           float *__restrict__ Xm, float *__restrict__ Wm) {
-    const int64_t nx = (int64_t)m * k, total = nx + (int64_t)k * n;
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-        if (e < nx) {
-            const int64_t r = e / k, c = e - r * k;
-            Xm[e] = flags[c] ? 0.0f : X[r * xsh + c];
-        } else {
-            const int64_t f = e - nx, r = f / n, c = f - r * n;
-            Wm[f] = flags[r] ? 0.0f : W[r * wsh + c];
-        }
+                                                           const uint32_t *__restrict__ bits, float *__restrict__ Xm,
+                                                           float *__restrict__ Wm) {
+    const int64_t row = blockIdx.x;
+    if (row < m) {
+        for (int c = threadIdx.x; c < k; c += 256) Xm[row * k + c] = bit_of(bits, c) ? 0.0f : X[row * xsh + c];
+    } else {
+        const int64_t r = row - m;
+        const bool z = bit_of(bits, r);
+        for (int c = threadIdx.x; c < n; c += 256) Wm[r * n + c] = z ? 0.0f : W[r * wsh + c];
     }
 }
 
@@ -83,9 +141,9 @@ __global__ __launch_bounds__(256) void outlier_mm_kernel(const float *__restrict
                                                          int64_t osh, int m, int n) {
     const int cnt = *count;
     if (cnt == 0) return;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= (int64_t)m * n) return;
-    const int i = (int)(e / n), j = (int)(e - (int64_t)i * n);
+    const int i = blockIdx.y;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m || j >= n) return;
     float acc = 0.0f;
     for (int t = 0; t < cnt; ++t) {
         const int c = idx[t];
@@ -94,49 +152,96 @@ __global__ __launch_bounds__(256) void outlier_mm_kernel(const float *__restrict
     O[(int64_t)i * osh + j] = __fadd_rn(O[(int64_t)i * osh + j], acc);
 }
 
+struct OutlierScratch {
+    uint32_t *partial, *bits;
+    int *rank, *idx;  // idx[0] = count
+    float *xm, *wm;   // X' / W' (fallback) or xo / wo (fast path)
+    int nchunks, nwords;
+};
+
+size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// [idx: count + list, k + 1 ints][bits][rank][partial][X' or xo][W' or wo]: the count's offset depends on
+// k only (qgemm_outlier_count)
+OutlierScratch scratch_view(void *scratch, int m, int k) {
+    OutlierScratch v;
+    v.nchunks = (m + kChunkRows - 1) / kChunkRows;
+    v.nwords = (k + 31) / 32;
+    char *p = static_cast<char *>(scratch);
+    v.idx = reinterpret_cast<int *>(p);
+    p += a256(sizeof(int) * ((size_t)k + 1));
+    v.bits = reinterpret_cast<uint32_t *>(p);
+    p += a256(sizeof(uint32_t) * v.nwords);
+    v.rank = reinterpret_cast<int *>(p);
+    p += a256(sizeof(int) * v.nwords);
+    v.partial = reinterpret_cast<uint32_t *>(p);
+    p += a256(sizeof(uint32_t) * (size_t)v.nchunks * v.nwords);
+    v.xm = reinterpret_cast<float *>(p);
+    p += a256(sizeof(float) * (size_t)m * k);
+    v.wm = reinterpret_cast<float *>(p);
+    return v;
+}
+
+// column mask, ranks, index list and count of X's outlier columns
+hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, hipStream_t s) {
+    const dim3 grid((unsigned)((k + kFlagCols - 1) / kFlagCols), (unsigned)v.nchunks);
+    const bool vec = (k % 4 == 0) && (xsh % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
+    if (vec) outlier_flags_kernel<true><<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords);
+    else outlier_flags_kernel<false><<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords);
+    outlier_index_kernel<<<1, 1024, 0, s>>>(v.partial, v.nchunks, v.nwords, v.bits, v.rank, v.idx);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 size_t outlier_scratch_bytes(int m, int n, int k) {
-    auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    return a256(sizeof(unsigned) * k) + a256(sizeof(int) * (k + 1)) + a256(sizeof(float) * (size_t)m * k) +
-           a256(sizeof(float) * (size_t)k * n);
+    const size_t nchunks = (size_t)(m + kChunkRows - 1) / kChunkRows, nwords = (size_t)(k + 31) / 32;
+    return a256(sizeof(uint32_t) * nchunks * nwords) + a256(sizeof(uint32_t) * nwords) + a256(sizeof(int) * nwords) +
+           a256(sizeof(int) * ((size_t)k + 1)) + a256(sizeof(float) * (size_t)m * k) +
+           a256(sizeof(float) * (size_t)k * (size_t)round_up(n, 256));
 }
 
-// Phase 1: flags, indices, X', W' into scratch; the caller then runs the int8 chain on (X', W') and
-// phase 2 (outlier_finish) adds the fp32 outlier products.
+// Fast path: flags + index, the masked single-pass pack, the 256-tile GEMM with the fp32 chain in its
+// epilogue.  hipErrorNotSupported (nothing launched) outside its envelope.
+hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
+                        PackedView va, PackedView vb, float range, hipStream_t s) {
+    if (!gemm_outlier_ok(m, n, (int)va.k_pad) || !pack_single_pass_outlier_ok(X, k, m, k, W, n, n)) return hipErrorNotSupported;
+    const OutlierScratch v = scratch_view(scratch, m, k);
+    const int64_t wo_ld = round_up(n, 256);
+    hipError_t e = outlier_scan(X, k, m, k, t, v, s);
+    if (e != hipSuccess) return e;
+    e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, v.bits, v.rank, v.idx, v.xm, v.wm, wo_ld,
+                                        s);
+    if (e == hipErrorNotSupported) return hipErrorUnknown;  // scan already enqueued: the envelope checks above disagree
+    if (e != hipSuccess) return e;
+    const float inv_r2 = 1.0f / (range * range);
+    return launch_gemm_dequant_outlier(va, vb, O, n, m, n, inv_r2, v.xm, v.wm, wo_ld, v.idx, s);
+}
+
+// Fallback phase 1: flags, indices, X', W' into scratch; the caller then runs the int8 chain on (X', W')
+// and phase 2 (outlier_finish) adds the fp32 outlier products.
 hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, float t,
                            void *scratch, float **Xm, float **Wm, hipStream_t s) {
-    auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    char *p = static_cast<char *>(scratch);
-    unsigned *flags = reinterpret_cast<unsigned *>(p);
-    int *idx = reinterpret_cast<int *>(p + a256(sizeof(unsigned) * k));
-    *Xm = reinterpret_cast<float *>(p + a256(sizeof(unsigned) * k) + a256(sizeof(int) * (k + 1)));
-    *Wm = *Xm + a256(sizeof(float) * (size_t)m * k) / sizeof(float);
-    hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned) * k, s);
+    const OutlierScratch v = scratch_view(scratch, m, k);
+    *Xm = v.xm;
+    *Wm = v.wm;
+    hipError_t e = outlier_scan(X, xsh, m, k, t, v, s);
     if (e != hipSuccess) return e;
-    const int rpb = 256;
-    outlier_cols_kernel<<<dim3((unsigned)((k + 255) / 256), (unsigned)((m + rpb - 1) / rpb)), 256, 0, s>>>(X, xsh, m, k,
-                                                                                                       t, rpb, flags);
-    outlier_index_kernel<<<1, 1024, 0, s>>>(flags, k, idx + 1, idx);
-    const int64_t total = (int64_t)m * k + (int64_t)k * n;
-    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 16384);
-    outlier_mask_kernel<<<blocks, 256, 0, s>>>(X, xsh, m, k, W, wsh, n, flags, *Xm, *Wm);
+    outlier_mask_kernel<<<(unsigned)(m + k), 256, 0, s>>>(X, xsh, m, k, W, wsh, n, v.bits, v.xm, v.wm);
     return hipGetLastError();
 }
 
 hipError_t outlier_finish(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, void *scratch,
                           float *O, int64_t osh, hipStream_t s) {
-    auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const int *idx = reinterpret_cast<const int *>(static_cast<char *>(scratch) + a256(sizeof(unsigned) * k));
-    outlier_mm_kernel<<<(unsigned)(((int64_t)m * n + 255) / 256), 256, 0, s>>>(X, xsh, W, wsh, idx + 1, idx, O, osh, m,
-                                                                              n);
+    const OutlierScratch v = scratch_view(scratch, m, k);
+    outlier_mm_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)m), 256, 0, s>>>(X, xsh, W, wsh, v.idx + 1, v.idx,
+                                                                                     O, osh, m, n);
     return hipGetLastError();
 }
 
 int outlier_count_slot(int k, const void *scratch, int *count_host) {
-    auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const int *idx = reinterpret_cast<const int *>(static_cast<const char *>(scratch) + a256(sizeof(unsigned) * k));
-    return (int)hipMemcpy(count_host, idx, sizeof(int), hipMemcpyDeviceToHost);
+    (void)k;  // the count leads the scratch
+    return (int)hipMemcpy(count_host, scratch, sizeof(int), hipMemcpyDeviceToHost);
 }
 
 }  // namespace qgemm

@@ -61,13 +61,31 @@ __device__ __forceinline__ void zero_words_block0(uint32_t *words, int n) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// LLM.int8() decomposition inside the pack (outlier.hip builds the mask): feature k of X is an outlier
+// column when bit k of `bits` is set.  The int8 chain runs on X' / W' = X / W with those columns /
+// rows zeroed, so the packs treat them as +0 (absmax candidates, the signed seed and the quantized
+// bytes alike, exactly as packing the zeroed copies), and the pass that holds the original values
+// in registers writes them out compactly for the fp32 part: xo[i * cnt + rank(k)] = X[i,k],
+// wo[rank(k) * wo_ld + j] = W[k,j], rank(k) = outlier columns below k.
+struct OutlierMask {
+    const uint32_t *bits;  // ceil(K/32) words
+    const int *rank;       // per word: set bits in the words below it
+    const int *count;      // outlier columns (device)
+    float *xo, *wo;
+    int64_t wo_ld;
+};
+__device__ __forceinline__ bool om_bit(const OutlierMask &om, int k) { return (om.bits[k >> 5] >> (k & 31)) & 1u; }
+
+// ------------------------------------------------------------------------------------------------
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
 // R > 0: each lane keeps R float4 chunks in registers (len <= 256*R), one HBM read.
 // R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
-template <int R>
+template <int R, bool kMask = false>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
-                                                   int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad) {
+                                                   int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
+                                                   const OutlierMask *om = nullptr) {
+    static_assert(!kMask || R > 0, "the outlier mask needs the register-resident rows");
     const int lane = threadIdx.x & 63;
     const int64_t row = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     if (row >= rows_pad) return;
@@ -81,7 +99,7 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     const float *srow = src + row * sh;
     const float4 *s4 = reinterpret_cast<const float4 *>(srow);
     const int nfull = len >> 2;  // complete float4 chunks
-    const float seed = srow[0];
+    float seed = srow[0];
 
     float p = -INFINITY;
     float4 v[R > 0 ? R : 1];
@@ -89,10 +107,55 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         // buffer loads on one per-lane offset; chunks >= nfull lie past the descriptor and read as zeros
         typedef int v4i_t __attribute__((ext_vector_type(4)));
         const auto rs = buf_rsrc(srow, (uint32_t)nfull * 16);
+        // the mask words (<= 128: two per lane) and their ranks, issued ahead of the row so that they have
+        // arrived with it (no round trip after the row's loads); chunk c needs word (4c) >> 5 = c >> 3
+        uint32_t mw2[2] = {0u, 0u};
+        int mr2[2] = {0, 0};
+        if constexpr (kMask) {
+            static_assert(R <= 16, "two mask words per lane cover len <= 4096");
+            const int nw = (len + 31) >> 5;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int wi = min(lane + h * kWave, nw - 1);
+                mw2[h] = om->bits[wi];
+                mr2[h] = om->rank[wi];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, 0);
             v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
+        }
+        if constexpr (kMask) {
+            // outlier columns: their values go to xo, X' holds +0 there (the seed included)
+            const int cnt = *om->count;
+            if (cnt > 0) {
+                if (om_bit(*om, 0)) seed = 0.0f;
+                float *xrow = om->xo + row * cnt;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int c = lane + j * kWave;
+                    // word (lane >> 3) + 8j lives in lane ((lane >> 3) + 8j) & 63, half j >> 3 (the
+                    // shuffles outside the branches: every lane active)
+                    const int src_lane = ((lane >> 3) + 8 * j) & 63;
+                    const uint32_t mw = (uint32_t)__shfl((int)mw2[j >> 3], src_lane, 64);
+                    const int mr = __shfl(mr2[j >> 3], src_lane, 64);
+                    if (c < nfull) {
+                        const int sh = (4 * c) & 31;
+                        const uint32_t nib = (mw >> sh) & 15u;
+                        if (nib) {
+                            float e4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                if ((nib >> e) & 1u) {
+                                    xrow[mr + __popc(mw & ((1u << (sh + e)) - 1u))] = e4[e];
+                                    e4[e] = 0.0f;
+                                }
+                            v[j] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+                        }
+                    }
+                }
+            }
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -563,15 +626,30 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
 // n = 8192 at K >= 2048, worse for wider W (n = 12288, 16384) and short K, where the 16-column pass stays.
 constexpr int kWs8Cols = 8;
 
+template <bool kMask = false>
 __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                    float range, float *__restrict__ scale, int8_t *__restrict__ q,
-                                                   int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */) {
+                                                   int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */,
+                                                   const OutlierMask *om = nullptr) {
     typedef int v4i_t __attribute__((ext_vector_type(4)));
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c2 = t & 1, rq = t >> 1;
     const int64_t n0 = (int64_t)strip * kWs8Cols;
     const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kWs8Cols) * 4));
     const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c2) * 4);
+    // mask words of this thread's rows (word (4 rq + 1024 i) >> 5 for every e) and their ranks, issued
+    // ahead of the strip's loads
+    uint32_t mw[4];
+    int mr[4];
+    if constexpr (kMask) {
+        const int nw = (k + 31) >> 5;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int wi = min((4 * rq + 1024 * i) >> 5, nw - 1);
+            mw[i] = om->bits[wi];
+            mr[i] = om->rank[wi];
+        }
+    }
     float4 v[4][4];  // [i][e]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -580,6 +658,24 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
             const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, 0);
             v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
+    bool seed_masked = false;
+    if constexpr (kMask) {
+        // outlier rows of W (outlier feature columns of X): their values go to wo, W' holds +0 there
+        if (*om->count > 0) {
+            seed_masked = om_bit(*om, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * rq + e + 1024 * i, b = r & 31;
+                    if (r < k && ((mw[i] >> b) & 1u)) {
+                        const int rk = mr[i] + __popc(mw[i] & ((1u << b) - 1u));
+                        *reinterpret_cast<float4 *>(om->wo + rk * om->wo_ld + n0 + 4 * c2) = v[i][e];
+                        v[i][e] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+        }
+    }
     // column candidates over rows >= 1 (row 0 is the seed)
     float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
 #pragma unroll
@@ -614,7 +710,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
         float pm = red[t];
 #pragma unroll
         for (int ww = 1; ww < 8; ++ww) pm = fmaxf(pm, red[ww * 8 + t]);  // -inf or >= +0: exact
-        const float cw = absmax_finish(w[n0 + t], pm);                  // seed = W[0, j]
+        const float cw = absmax_finish(seed_masked ? 0.0f : w[n0 + t], pm);  // seed = W[0, j] (W'[0, j])
         s_sh[t] = inv_divide(range, cw);
         scale[n0 + t] = cw;
     }
@@ -642,11 +738,12 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     }
 }
 
-template <int kWavesPerEu>
+template <int kWavesPerEu, bool kMask = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu, kWavesPerEu))) void pack_single_pass8_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
-    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero) {
+    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero,
+    OutlierMask om = OutlierMask{}) {
     __shared__ float red[8 * 8 + 8];
     const int bid = blockIdx.x;
     zero_words_block0(zero_words, nzero);
@@ -655,7 +752,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         // blocks b, b+8, ... run on one XCD: XCD-contiguous strip ranges (bijective for any nstrips)
         const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
         const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-        pack_w_strip8_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, red);
+        pack_w_strip8_body<kMask>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kWs8Cols;
         for (int64_t i = threadIdx.x; i < (int64_t)kWs8Cols * k_pad / 16; i += 512)
@@ -663,7 +760,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         if (threadIdx.x < kWs8Cols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
         const int64_t xb = bid - nstrips - npad;  // rows 8xb + (t>>6): two 4-row groups of the 256-thread body
-        pack_rows_vec_body<16>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad);
+        pack_rows_vec_body<16, kMask>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om);
     }
 }
 
@@ -776,6 +873,27 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
                                                                          outx.k_pad, w, wsh, n, outw.scale, outw.q,
                                                                          outw.rows_pad, nstrips, range, zero_words,
                                                                          nzero);
+    return hipGetLastError();
+}
+
+bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, const float *w, int64_t wsh, int n) {
+    return k >= 1 && k <= kWsMaxK && !(k & 3) && rows_vec_ok(x, xsh, 1, m) && cols_vec_ok(w, wsh, n) &&
+           n % kWs8Cols == 0 && ((int64_t)k * wsh + kWs8Cols) * 4 < ((int64_t)1 << 31);
+}
+
+hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
+                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *bits,
+                                           const int *rank, const int *count, float *xo, float *wo, int64_t wo_ld,
+                                           hipStream_t stream) {
+    if (!pack_single_pass_outlier_ok(x, xsh, m, k, w, wsh, n) || (reinterpret_cast<uintptr_t>(wo) & 15) || (wo_ld & 3))
+        return hipErrorNotSupported;
+    const int nstrips = n / kWs8Cols;
+    const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
+    const int nx = (int)(outx.rows_pad / 8);
+    const OutlierMask om{bits, rank, count, xo, wo, wo_ld};
+    pack_single_pass8_kernel<5, true><<<nstrips + npad + nx, 512, 0, stream>>>(
+        x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad, nstrips,
+        range, nullptr, 0, om);
     return hipGetLastError();
 }
 

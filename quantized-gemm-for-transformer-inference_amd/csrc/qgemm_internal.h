@@ -106,6 +106,14 @@ hipError_t launch_pack_single_pass(const float *x, int64_t xsh, int m, int k, Pa
 hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
                                         int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind,
                                         uint32_t *zero_words = nullptr, int nzero = 0);
+// The single-pass pack (8-column W strips) of the LLM.int8() decomposition's int8 part: outlier columns
+// of X (bit k of `bits`) / rows of W packed as +0, their values written compactly to xo [m][cnt] / wo
+// [cnt][wo_ld] (outlier.hip).  hipErrorNotSupported outside the single pass's envelope (K % 4 == 0 too).
+bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, const float *w, int64_t wsh, int n);
+hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
+                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *bits,
+                                           const int *rank, const int *count, float *xo, float *wo, int64_t wo_ld,
+                                           hipStream_t stream);
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
@@ -122,6 +130,13 @@ size_t gemm_ticket_bytes(int m, int n, int k);
 hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *C, int64_t csh, int64_t csw,
                                int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
                                const float *bias = nullptr, bool relu = false, bool tickets_zeroed = false);
+// The LLM.int8() decomposition's GEMM: int8 part + the outlier columns' fp32 products in the epilogue
+// (xo [m][cnt], wo [cnt][wo_ld], wo_ld a multiple of 256, cnt = *ocount).  Only where the plan is the
+// 256-tile GEMM without split-K (gemm_outlier_ok); hipErrorNotSupported otherwise.
+bool gemm_outlier_ok(int m, int n, int k);
+hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b, float *C, int64_t csh, int m, int n,
+                                       float inv_r2, const float *xo, const float *wo, int64_t wo_ld, const int *ocount,
+                                       hipStream_t stream);
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
                            hipStream_t stream);
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,
@@ -150,6 +165,10 @@ hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t 
 hipError_t outlier_finish(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, void *scratch,
                           float *O, int64_t osh, hipStream_t s);
 int outlier_count_slot(int k, const void *scratch, int *count_host);
+// fast path (flags, indices, masked single-pass pack, GEMM with the fp32 chain in its epilogue) into the
+// packed views va / vb; hipErrorNotSupported (nothing launched) outside its envelope (row-major operands)
+hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
+                        PackedView va, PackedView vb, float range, hipStream_t s);
 // The encoder counterpart (encoder.hip).
 struct Encoder;
 uint64_t encoder_weight_seed(uint64_t base, int block, int kind, int head);

@@ -37,6 +37,33 @@ def test_outlier_decomposition_bit_exact(qg, oracle, device, M, N, K, cols):
     assert_bits_equal(C.cpu().numpy(), want, f"outlier decomposition {M}x{N}x{K}")
 
 
+# shapes on the fast path (>= 160 256-tiles, row-major, K % 4 == 0, K <= 4096, N % 8 == 0): the masked
+# single-pass pack and the chain in the GEMM epilogue; ragged M / N / K, mask-word edges, column 0 (the
+# absmax seed) and the last column
+@pytest.mark.parametrize("M,N,K,cols", [(2500, 4000, 132, [0, 1, 31, 32, 63, 131]),
+                                        (2560, 4096, 1024, list(range(7, 1024, 37))),
+                                        (2560, 4000, 64, list(range(64)))])
+def test_outlier_fast_path_bit_exact(qg, oracle, device, M, N, K, cols):
+    X, W = _with_outliers(oracle, M, N, K, cols, 9)
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    assert cnt == wcnt == len(cols)
+    assert_bits_equal(C.cpu().numpy(), want, f"outlier fast path {M}x{N}x{K}")
+
+
+def test_outlier_fast_path_nan_and_none(qg, oracle, device):
+    X, W = oracle.inputs(2560, 4096, 128, 10)
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
+    assert cnt == 0
+    assert_bits_equal(C.cpu().numpy(), oracle.quantized_mm(X, W), "fast path, no outliers")
+    X[17, 0] = np.nan
+    X[2000, 127] = -9.0
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    assert cnt == wcnt == 2
+    assert_bits_equal(C.cpu().numpy(), want, "fast path, NaN column")
+
+
 def test_no_outliers_is_the_plain_path(qg, oracle, device):
     X, W = oracle.inputs(256, 300, 700, 6)
     C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
