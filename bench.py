@@ -38,6 +38,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 PRACTICAL_INT8_TOPS = 4116.0
 PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12
 PEAK_HBM_GBS = 8000.0
+OUTLIER_COLS = 8
+OUTLIER_THRESHOLD = 6.0
 
 CONFIGS = {
     # name: (M, N, K, description)  -- BASELINE.json configs
@@ -45,6 +47,10 @@ CONFIGS = {
     "c3_up": (2048, 16384, 4096, "FFN up 2048x4096->16384 (BASELINE configs[2])"),
     "c3_down": (2048, 4096, 16384, "FFN down 2048x16384->4096 (BASELINE configs[2])"),
     "c4_shard": (8192, 4096, 4096, "M=65536 K=N=4096 / 8 GPUs, one 8192-row shard (BASELINE configs[3])"),
+    # the LLM.int8() decomposition (qgemm_mm_outlier) at the headline shape, X with
+    # OUTLIER_COLS outlier feature columns (|x| 7..60 in every 50th row; threshold 6)
+    "c2_outlier": (4096, 4096, 4096, "M=N=K=4096 LLM.int8() outlier decomposition (qgemm_mm_outlier, threshold 6, "
+                   "8 outlier feature columns)"),
     # encoder forward: (seq, d_model, n_heads, d_ff, n_blocks)
     "c5_encoder": (512, 1024, 16, 4096, 2, "encoder forward d_model=1024 seq=512 (BASELINE configs[4]), 16 heads, "
                    "d_ff 4096, 2 blocks; quantized Q/K/V, W_O, FFN linears"),
@@ -135,20 +141,32 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(M, N, K, target_s):
+def outlier_columns(K):
+    """The c2_outlier workload's outlier feature columns (spread over K) and their rows (every 50th)."""
+    return [(K // OUTLIER_COLS) * c + 7 * c + 3 for c in range(OUTLIER_COLS)], 50
+
+
+def cpu_baseline(M, N, K, target_s, outlier=False):
     """Time the oracle's quantized chain (and the unquantized fp32 GEMM) on the host cores.
 
     The sample is the full workload repeated until ~target_s of CPU time (the oracle runs a whole
-    M=N=K=4096 chain in well under a second on 16 cores); the fp32 path runs on a row sample."""
+    M=N=K=4096 chain in well under a second on 16 cores); the fp32 path runs once on the full problem."""
     from oracle import oracle as O
     O.build()
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     X, W = O.uniform((M, K), 0), O.uniform((K, N), 1)
+    if outlier:
+        cols, every = outlier_columns(K)
+        for c in cols:
+            X[::every, c] = 30.0
+        run = lambda: O.mm_outlier(X, W, OUTLIER_THRESHOLD)  # noqa: E731
+    else:
+        run = lambda: O.quantized_mm(X, W)  # noqa: E731
     O.quantized_mm(X[:64], W)  # warm the pool / pages
     reps, tq = 0, 0.0
     while tq < target_s and reps < 200:
         t0 = time.perf_counter()
-        O.quantized_mm(X, W)
+        run()
         tq += time.perf_counter() - t0
         reps += 1
     # the unquantized fp32 op_mm on the FULL problem, once (sequential-k fmaf; ~0.6 s at 4096^3 on 16 threads)
@@ -162,11 +180,20 @@ def cpu_baseline(M, N, K, target_s):
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
         "kind": "port",
-        "sample": f"oracle/ C restatement of the reference chain (op_mm.cuh:67-101), full {M}x{N}x{K} "
+        "sample": ("oracle/ C restatement of the LLM.int8() decomposition (oracle_mm_outlier)" if outlier else
+                   "oracle/ C restatement of the reference chain (op_mm.cuh:67-101)") + f", full {M}x{N}x{K} "
                   f"problem x{reps} = {tq:.1f} s on {threads} OpenMP threads; unquantized fp32 op_mm "
                   f"(the reference's op_mm<float>, sequential-k fmaf) on the full problem once: {tf:.2f} s",
         "unquantized_gemms_per_s": 1.0 / tf,
     }
+
+
+def ctypes_count(L, K, ws):
+    import ctypes
+    c = ctypes.c_int(-1)
+    if L.qgemm_outlier_count(K, ws.data_ptr(), ctypes.byref(c)) != 0:
+        raise RuntimeError("qgemm_outlier_count failed")
+    return c.value
 
 
 def c4_node(args, qg, dev, world, rank, distributed):
@@ -261,7 +288,18 @@ def main():
     X = qg.fill_uniform(torch.empty((M, K), device=dev), seed=2 * (1000 + rank))
     W = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 1000 + 1)
     O = torch.empty((M, N), device=dev)
-    ws = torch.empty(L.op_mm_quantize_workspace_size(M, N, K), dtype=torch.uint8, device=dev)
+    outlier = args.config == "c2_outlier"
+    if outlier:
+        cols, every = outlier_columns(K)
+        g = torch.Generator(device="cpu").manual_seed(rank)
+        for c in cols:
+            rows = X[::every, c]
+            mag = 7.0 + 53.0 * torch.rand(rows.numel(), generator=g)
+            sign = torch.where(torch.rand(rows.numel(), generator=g) < 0.5, -1.0, 1.0)
+            X[::every, c] = (mag * sign).to(dev)
+        ws = torch.empty(L.qgemm_mm_outlier_workspace_size(M, N, K), dtype=torch.uint8, device=dev)
+    else:
+        ws = torch.empty(L.op_mm_quantize_workspace_size(M, N, K), dtype=torch.uint8, device=dev)
     s = qg._stream(dev)
     range_ = 127.0
     hip = HipEvents(2 * args.steps)
@@ -275,10 +313,14 @@ def main():
         # the drop-in call: op_mm_quantize on caller memory (explicit workspace, torch's stream)
         if i is not None and mode != "none" and i % every == 0:
             L.qgemm_set_gemm_events(hip.ev[2 * i], hip.ev[2 * i + 1])
-        rc = L.op_mm_quantize_ws(X.data_ptr(), K, 1, W.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, range_,
-                                 ws.data_ptr(), ws.numel(), s)
+        if outlier:
+            rc = L.qgemm_mm_outlier(X.data_ptr(), W.data_ptr(), O.data_ptr(), M, N, K, OUTLIER_THRESHOLD,
+                                    ws.data_ptr(), ws.numel(), s)
+        else:
+            rc = L.op_mm_quantize_ws(X.data_ptr(), K, 1, W.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, range_,
+                                     ws.data_ptr(), ws.numel(), s)
         if rc:
-            raise RuntimeError(f"op_mm_quantize_ws returned {rc}")
+            raise RuntimeError(f"{'qgemm_mm_outlier' if outlier else 'op_mm_quantize_ws'} returned {rc}")
 
     for _ in range(args.warmup):
         step()
@@ -323,7 +365,10 @@ def main():
         "dtype": "int8",
         "data": "synthetic U(-1,1) fp32 inputs (seeded counter-based generator, generated in HBM)",
         "config": {
-            "workload": f"op_mm_quantize fp32->fp32, {desc}: pack X + pack W + int8 MFMA GEMM/dequant per step",
+            "workload": (f"qgemm_mm_outlier fp32->fp32, {desc}: outlier flags + index, masked pack of X and W, "
+                         "int8 MFMA GEMM/dequant with the outlier columns' fp32 chain in its epilogue, per step"
+                         if outlier else
+                         f"op_mm_quantize fp32->fp32, {desc}: pack X + pack W + int8 MFMA GEMM/dequant per step"),
             "M": M, "N": N, "K": K, "global_M": M * world, "range": range_,
             "parallelism": f"M-shard x{world} (replicated W, no collective)",
         },
@@ -341,7 +386,8 @@ def main():
             "traffic_unit": "bytes per launch (HBM + Infinity Cache fill, FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
             "alg_bytes": M * K + N * K + 4 * M * N + 4 * (M + N),
-            "kernel": "gemm_i8_pp<1> (int8 16x16x64 MFMA GEMM, ping-pong schedule, fused dequant epilogue)",
+            "kernel": "gemm_i8_pp<1> (int8 16x16x64 MFMA GEMM, ping-pong schedule, fused dequant epilogue"
+                      + (" + outlier fp32 chain)" if outlier else ")"),
             "ceiling_measured": {
                 "value": PRACTICAL_INT8_TOPS, "frac": round(achieved / PRACTICAL_INT8_TOPS, 4),
                 "note": "bare v_mfma_i32_16x16x64_i8 issue, operands in registers, no VALU in the loop, every CU, "
@@ -389,7 +435,10 @@ def main():
                                          "timing_quantize.cu:67-70); the others fp64 on the device")
         del C
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(M, N, K, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(M, N, K, args.cpu_seconds, outlier=outlier)
+    if outlier and rank == 0:
+        cnt = ctypes_count(L, K, ws)
+        result["config"]["outlier_columns"] = cnt
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:
