@@ -49,6 +49,10 @@ CONFIGS = {
     "c4_shard": (8192, 4096, 4096, "M=65536 K=N=4096 / 8 GPUs, one 8192-row shard (BASELINE configs[3])"),
     # the LLM.int8() decomposition (qgemm_mm_outlier) at the headline shape, X with
     # OUTLIER_COLS outlier feature columns (|x| 7..60 in every 50th row; threshold 6)
+    # the weight-cache drop-in (op_mm_quantize_prepacked) at the headline shape, W packed
+    # once before the timed region, X quantized in every step
+    "c2_prepacked": (4096, 4096, 4096, "M=N=K=4096 with W prepacked once (op_mm_quantize_prepacked: pack X + "
+                     "int8 GEMM/dequant per step)"),
     "c2_outlier": (4096, 4096, 4096, "M=N=K=4096 LLM.int8() outlier decomposition (qgemm_mm_outlier, threshold 6, "
                    "8 outlier feature columns)"),
     # encoder forward: (seq, d_model, n_heads, d_ff, n_blocks)
@@ -289,6 +293,7 @@ def main():
     W = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 1000 + 1)
     O = torch.empty((M, N), device=dev)
     outlier = args.config == "c2_outlier"
+    prepacked = args.config == "c2_prepacked"
     if outlier:
         cols, every = outlier_columns(K)
         g = torch.Generator(device="cpu").manual_seed(rank)
@@ -298,6 +303,9 @@ def main():
             sign = torch.where(torch.rand(rows.numel(), generator=g) < 0.5, -1.0, 1.0)
             X[::every, c] = (mag * sign).to(dev)
         ws = torch.empty(L.qgemm_mm_outlier_workspace_size(M, N, K), dtype=torch.uint8, device=dev)
+    elif prepacked:
+        pb = qg.pack_b(W)  # the weight cache: quantized once, outside the timed region
+        ws = torch.empty(L.op_mm_quantize_prepacked_workspace_size(M, N, K), dtype=torch.uint8, device=dev)
     else:
         ws = torch.empty(L.op_mm_quantize_workspace_size(M, N, K), dtype=torch.uint8, device=dev)
     s = qg._stream(dev)
@@ -316,11 +324,14 @@ def main():
         if outlier:
             rc = L.qgemm_mm_outlier(X.data_ptr(), W.data_ptr(), O.data_ptr(), M, N, K, OUTLIER_THRESHOLD,
                                     ws.data_ptr(), ws.numel(), s)
+        elif prepacked:
+            rc = L.op_mm_quantize_prepacked_ws(X.data_ptr(), K, pb.buf.data_ptr(), O.data_ptr(), N, M, N, K,
+                                               ws.data_ptr(), ws.numel(), s)
         else:
             rc = L.op_mm_quantize_ws(X.data_ptr(), K, 1, W.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, range_,
                                      ws.data_ptr(), ws.numel(), s)
         if rc:
-            raise RuntimeError(f"{'qgemm_mm_outlier' if outlier else 'op_mm_quantize_ws'} returned {rc}")
+            raise RuntimeError(f"drop-in call ({args.config}) returned {rc}")
 
     for _ in range(args.warmup):
         step()
@@ -368,6 +379,7 @@ def main():
             "workload": (f"qgemm_mm_outlier fp32->fp32, {desc}: outlier flags + index, masked pack of X and W, "
                          "int8 MFMA GEMM/dequant with the outlier columns' fp32 chain in its epilogue, per step"
                          if outlier else
+                         f"op_mm_quantize_prepacked fp32->fp32, {desc}" if prepacked else
                          f"op_mm_quantize fp32->fp32, {desc}: pack X + pack W + int8 MFMA GEMM/dequant per step"),
             "M": M, "N": N, "K": K, "global_M": M * world, "range": range_,
             "parallelism": f"M-shard x{world} (replicated W, no collective)",
@@ -436,6 +448,8 @@ def main():
         del C
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(M, N, K, args.cpu_seconds, outlier=outlier)
+        if prepacked:
+            result["cpu_baseline"]["note"] = "the reference chain re-quantizes W every call (it has no weight cache)"
     if outlier and rank == 0:
         cnt = ctypes_count(L, K, ws)
         result["config"]["outlier_columns"] = cnt

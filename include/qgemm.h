@@ -78,6 +78,16 @@ QGEMM_API int qgemm_pack_b(const float *B, int64_t b_stride_h, int64_t b_stride_
 /* int8 x int8 -> int32 MFMA GEMM with the fused dequantize epilogue (op_mm.cuh:92-99). */
 QGEMM_API int qgemm_mm_packed(const void *packed_a, const void *packed_b, float *C, int64_t c_stride_h,
                     int64_t c_stride_w, int m, int n, int k, float range, void *stream);
+/* The weight-cache form of the drop-in (op_mm_quantize_prepacked): B was packed once
+ * with qgemm_pack_b(range 127); every call quantizes A (op_mm.cuh:76-77, 82-87) and runs the int8 GEMM
+ * with the fused dequantize (op_mm.cuh:92-99) -- bit-identical to op_mm_quantize(A, B, C, m, n, k) on the
+ * B that was packed.  A: m x k (row stride a_stride_h, unit column stride), C: m x n (row stride
+ * c_stride_h).  The plain form uses the library's workspace and the null stream. */
+QGEMM_API int op_mm_quantize_prepacked(const float *A, const void *packed_b, float *C, int m, int n, int k);
+QGEMM_API size_t op_mm_quantize_prepacked_workspace_size(int m, int n, int k);
+QGEMM_API int op_mm_quantize_prepacked_ws(const float *A, int64_t a_stride_h, const void *packed_b, float *C,
+                                int64_t c_stride_h, int m, int n, int k, void *workspace, size_t ws_bytes,
+                                void *stream);
 /* Debug/parity view of the raw int32 accumulator (op_mm<int8_t,int>, op_mm.cuh:92-93):
  * Acc is m x n row-major int32. */
 QGEMM_API int qgemm_mm_packed_i32(const void *packed_a, const void *packed_b, int32_t *Acc, int m, int n, int k,

@@ -51,6 +51,9 @@ EXPORTED_SYMBOLS = (
     "qgemm_error_stats",
     "qgemm_linear_workspace_size",
     "qgemm_linear",
+    "op_mm_quantize_prepacked",
+    "op_mm_quantize_prepacked_workspace_size",
+    "op_mm_quantize_prepacked_ws",
     "qgemm_softmax_rows",
     "qgemm_add_layernorm_rows",
     "qgemm_encoder_create",
@@ -137,6 +140,12 @@ def load() -> ctypes.CDLL:
         L.qgemm_linear_workspace_size.restype = sz
         L.qgemm_linear.argtypes = [vp, i64, i32, i32, vp, i32, vp, i32, vp, i64, vp, sz, vp]
         L.qgemm_linear.restype = i32
+        L.op_mm_quantize_prepacked.argtypes = [vp, vp, vp, i32, i32, i32]
+        L.op_mm_quantize_prepacked.restype = i32
+        L.op_mm_quantize_prepacked_workspace_size.argtypes = [i32, i32, i32]
+        L.op_mm_quantize_prepacked_workspace_size.restype = sz
+        L.op_mm_quantize_prepacked_ws.argtypes = [vp, i64, vp, vp, i64, i32, i32, i32, vp, sz, vp]
+        L.op_mm_quantize_prepacked_ws.restype = i32
         L.qgemm_softmax_rows.argtypes = [vp, vp, i64, i32, f32, vp]
         L.qgemm_softmax_rows.restype = i32
         L.qgemm_add_layernorm_rows.argtypes = [vp, vp, vp, i64, i32, vp]
@@ -428,6 +437,25 @@ def linear(X, pw: Packed, bias=None, relu: bool = False, Y=None):
     _check("qgemm_linear", L.qgemm_linear(X.data_ptr(), X.stride(0), M, K, pw.buf.data_ptr(), N, b, 1 if relu else 0,
                                           Y.data_ptr(), Y.stride(0), ws.data_ptr(), ws.numel(), _stream(X.device)))
     return Y
+
+
+def op_mm_quantize_prepacked(A, pb: Packed, C=None):
+    """The weight-cache drop-in: C = op_quantized_mm(A, W) with W packed once by
+    pack_b; A quantized on every call (op_mm.cuh:76-77, 82-87), then the int8 GEMM + dequantize."""
+    import torch
+    _require_device_f32(A, "A")
+    assert A.stride(1) == 1 and A.shape[1] == pb.k
+    M, K = A.shape
+    N = pb.rows
+    if C is None:
+        C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    assert C.shape == (M, N) and C.stride(1) == 1
+    L = load()
+    ws = torch.empty(max(1, L.op_mm_quantize_prepacked_workspace_size(M, N, K)), dtype=torch.uint8, device=A.device)
+    _check("op_mm_quantize_prepacked_ws",
+           L.op_mm_quantize_prepacked_ws(A.data_ptr(), A.stride(0), pb.buf.data_ptr(), C.data_ptr(), C.stride(0), M, N,
+                                         K, ws.data_ptr(), ws.numel(), _stream(A.device)))
+    return C
 
 
 def softmax_rows(S, scale: float = 1.0, P=None):

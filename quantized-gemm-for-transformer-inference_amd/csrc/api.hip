@@ -267,6 +267,25 @@ size_t qgemm_linear_workspace_size(int m, int n, int k) {
     return align256(gemm_scratch_bytes(m, n, k)) + align256(packed_bytes(m, k));
 }
 
+size_t op_mm_quantize_prepacked_workspace_size(int m, int n, int k) { return qgemm_linear_workspace_size(m, n, k); }
+
+int op_mm_quantize_prepacked_ws(const float *A, int64_t a_stride_h, const void *packed_b, float *C, int64_t c_stride_h,
+                                int m, int n, int k, void *workspace, size_t ws_bytes, void *stream) {
+    // op_mm.cuh:71-72: shape agreement and device residency are asserted by the reference
+    if (!A || !packed_b || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    return qgemm_linear(A, a_stride_h, m, k, packed_b, n, nullptr, 0, C, c_stride_h, workspace, ws_bytes, stream);
+}
+
+int op_mm_quantize_prepacked(const float *A, const void *packed_b, float *C, int m, int n, int k) {
+    if (!A || !packed_b || !C || !dims_ok(m, n, k)) return err(hipErrorInvalidValue);
+    if (m == 0 || n == 0) return 0;
+    const size_t need = qgemm_linear_workspace_size(m, n, k);
+    void *ws = nullptr;
+    hipError_t e = cached_workspace(need, &ws);
+    if (e != hipSuccess) return err(e);
+    return op_mm_quantize_prepacked_ws(A, k, packed_b, C, n, m, n, k, ws, need, nullptr);
+}
+
 int qgemm_softmax_rows(const float *S, float *P, int64_t rows, int w, float scale, void *stream) {
     if (!S || !P) return err(hipErrorInvalidValue);
     return err(launch_softmax_rows(S, P, rows, w, scale, static_cast<hipStream_t>(stream)));

@@ -273,6 +273,24 @@ def test_explicit_workspace_and_prepacked_weights(qg, oracle, device):
         assert_bits_equal(O2.cpu().numpy(), want, "prepacked B")
 
 
+@pytest.mark.parametrize("M,N,K", [(384, 512, 640), (1000, 300, 1), (4096, 4096, 4096), (512, 1024, 4096)])
+def test_op_mm_quantize_prepacked(qg, oracle, device, M, N, K):
+    """op_mm_quantize_prepacked (W packed once, A quantized per call) is the drop-in bit
+    for bit -- the 4096^3 headline (every output) and a split-K shape included; both C-ABI forms."""
+    X, W = oracle.inputs(M, N, K, 57)
+    want = oracle.quantized_mm(X, W)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    pb = qg.pack_b(Wd)
+    for _ in range(2):
+        O = qg.op_mm_quantize_prepacked(Xd, pb)
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"op_mm_quantize_prepacked_ws {M}x{N}x{K}")
+    O2 = torch.full((M, N), float("nan"), device=device)
+    assert qg.load().op_mm_quantize_prepacked(Xd.data_ptr(), pb.buf.data_ptr(), O2.data_ptr(), M, N, K) == 0
+    torch.cuda.synchronize()
+    assert_bits_equal(O2.cpu().numpy(), want, f"op_mm_quantize_prepacked {M}x{N}x{K}")
+
+
 def test_unquantized_gemm_matches_reference_order(qg, oracle, device):
     """qgemm_mm_fp32 is the reference's op_mm<float,float>: sequential-k fmaf, bit-exact (on the f32
     MFMA: every tile configuration, k % 4 / k % 32 tails, K = 1)."""
