@@ -89,3 +89,35 @@ def test_decomposition_reduces_quantization_error(qg, oracle, device):
     e_plain = np.abs(ref - plain).mean()
     e_dec = np.abs(ref - C.cpu().numpy()).mean()
     assert e_dec < 0.75 * e_plain, (e_dec, e_plain)  # measured 0.117 vs 0.203
+
+
+def test_outlier_graph_capture_and_repeat(qg, oracle, device):
+    """qgemm_mm_outlier makes no allocation and no host sync (the outlier count stays on the device), so the
+    four fast-path launches (flags, index, masked pack, GEMM with the chain) can be captured in a HIP graph
+    and replayed; and 20 eager calls on one workspace give the same bits every time (race screen of the
+    partial-mask / rank / compact-value hand-offs)."""
+    import torch
+    M, N, K = 2560, 4096, 512
+    X, W = _with_outliers(oracle, M, N, K, [0, 5, 77, 300, 511], 12)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    L = qg.load()
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    ws = torch.empty(L.qgemm_mm_outlier_workspace_size(M, N, K), dtype=torch.uint8, device=device)
+    O = torch.full((M, N), float("nan"), device=device)
+    s = torch.cuda.Stream(device)
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            assert L.qgemm_mm_outlier(Xd.data_ptr(), Wd.data_ptr(), O.data_ptr(), M, N, K, 6.0, ws.data_ptr(),
+                                      ws.numel(), s.cuda_stream) == 0
+    for _ in range(3):
+        O.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, "outlier graph replay")
+    for i in range(20):
+        assert L.qgemm_mm_outlier(Xd.data_ptr(), Wd.data_ptr(), O.data_ptr(), M, N, K, 6.0, ws.data_ptr(), ws.numel(),
+                                  s.cuda_stream) == 0
+        s.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"outlier repeat {i}")
+    assert wcnt == 5

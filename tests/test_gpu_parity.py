@@ -394,6 +394,30 @@ def test_hip_graph_capture_replays_bit_exact(qg, oracle, device):
             assert_bits_equal(O.cpu().numpy(), want, f"graph replay {M}x{N}x{K}")
 
 
+def test_prepacked_graph_capture(qg, oracle, device):
+    """op_mm_quantize_prepacked_ws (caller workspace, W packed once outside the graph) captured and replayed."""
+    L = qg.load()
+    for (M, N, K) in [(384, 512, 640), (512, 1024, 4096)]:
+        X, W = oracle.inputs(M, N, K, 113)
+        want = oracle.quantized_mm(X, W)
+        Xd, Wd = _dev(X, device), _dev(W, device)
+        pb = qg.pack_b(Wd)
+        ws = torch.empty(max(1, L.op_mm_quantize_prepacked_workspace_size(M, N, K)), dtype=torch.uint8, device=device)
+        O = torch.full((M, N), float("nan"), device=device)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream(device)
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                assert L.op_mm_quantize_prepacked_ws(Xd.data_ptr(), K, pb.buf.data_ptr(), O.data_ptr(), N, M, N, K,
+                                                     ws.data_ptr(), ws.numel(), s.cuda_stream) == 0
+        for _ in range(3):
+            O.fill_(float("nan"))
+            g.replay()
+            torch.cuda.synchronize()
+            assert_bits_equal(O.cpu().numpy(), want, f"prepacked graph replay {M}x{N}x{K}")
+
+
 def test_concurrent_streams_with_own_workspaces(qg, oracle, device):
     L = qg.load()
     M, N, K = 512, 1024, 4096  # split-K plan on both streams
