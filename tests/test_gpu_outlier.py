@@ -121,3 +121,20 @@ def test_outlier_graph_capture_and_repeat(qg, oracle, device):
         s.synchronize()
         assert_bits_equal(O.cpu().numpy(), want, f"outlier repeat {i}")
     assert wcnt == 5
+
+
+@pytest.mark.parametrize("M,N,K,t", [(2560, 4096, 256, 0.0),      # threshold 0: every column an outlier (fast path)
+                                     (2560, 4004, 256, 6.0),      # N % 8 != 0: the materialising fallback
+                                     (2561, 4096, 258, 6.0),      # K % 4 != 0: fallback, ragged M
+                                     (2560, 4096, 256, float("inf"))])  # nothing is an outlier: the plain path
+def test_outlier_edges(qg, oracle, device, M, N, K, t):
+    X, W = _with_outliers(oracle, M, N, K, [1, 100, K - 1], 13)
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), t)
+    want, wcnt = oracle.mm_outlier(X, W, t)
+    assert cnt == wcnt
+    if t == 0.0:
+        assert cnt == K
+    if t == float("inf"):
+        assert cnt == 0
+        assert_bits_equal(want, oracle.quantized_mm(X, W), "oracle: no outliers = plain path")
+    assert_bits_equal(C.cpu().numpy(), want, f"outlier edge {M}x{N}x{K} t={t}")
