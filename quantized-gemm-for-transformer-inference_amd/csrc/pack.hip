@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void pack_rows_generic_kernel(const float *__r
 // lane owns 4 columns (VEC: contiguous float4 -> 1 KiB per wave load; else stride-64 scalars).
 constexpr int kColBlock = 256;  // columns per pass-1 block
 
-template <bool VEC>
+template <bool VEC, int kUnroll = 8>
 __device__ __forceinline__ void colmax_body(int cb, int part, const float *__restrict__ src, int64_t sh, int len,
                                             int cols, uint32_t *__restrict__ partial, int64_t rows_pad,
                                             float *red /* 4 x 256 floats of LDS */) {
@@ -329,7 +329,7 @@ __device__ __forceinline__ void colmax_body(int cb, int part, const float *__res
         const int64_t c = c0 + lane * 4;
         if (c < cols) {
             const float *base = src + c;
-#pragma unroll 8
+#pragma unroll(kUnroll)
             for (int64_t r = r0; r < r1; ++r) {
                 const float4 x = *reinterpret_cast<const float4 *>(base + r * sh);
                 p0 = cand_max(p0, x.x);

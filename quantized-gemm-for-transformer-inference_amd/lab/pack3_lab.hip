@@ -21,6 +21,20 @@ static void pass2(const float *W, int k, int n, PackedView vw, hipStream_t s) {
                                                    vw.k_pad);
 }
 
+// pass-1 variants: colmax unroll depth U; XF = X-row blocks dispatched first
+template <int U, bool XF>
+__global__ __launch_bounds__(256) void fused_var(const float *__restrict__ a, int64_t ash, int m, int k,
+                                                 float *__restrict__ a_scale, int8_t *__restrict__ a_q,
+                                                 int64_t a_rows_pad, int64_t k_pad, const float *__restrict__ b,
+                                                 int64_t bsh, int n, uint32_t *__restrict__ b_partial,
+                                                 int64_t b_rows_pad, int col_blocks, int ncol, int nrow, float range) {
+    __shared__ float red[4 * 256];
+    int bid = blockIdx.x;
+    if (XF) bid = bid < nrow ? ncol + bid : bid - nrow;
+    if (bid < ncol) colmax_body<true, U>(bid % col_blocks, bid / col_blocks, b, bsh, k, n, b_partial, b_rows_pad, red);
+    else pack_row_block_body(bid - ncol, a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad, red);
+}
+
 int main(int argc, char **argv) {
     int m = argc > 1 ? atoi(argv[1]) : 2048, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 16384;
     int reps = argc > 4 ? atoi(argv[4]) : 10;
@@ -42,6 +56,12 @@ int main(int argc, char **argv) {
     fused(); CK(launch_pack_cols_pass2(W, n, k, n, 127.f, vw, s0)); CK(hipStreamSynchronize(s0));
     const size_t part_bytes = (size_t)vw.parts * vw.rows_pad * 4;
     auto sync_partials = [&]() { CK(hipMemcpyAsync(vw2.scratch, vw.scratch, part_bytes, hipMemcpyDeviceToDevice, s0)); };
+    const int col_blocks = (n + kColBlock - 1) / kColBlock, ncol = col_blocks * (int)vw.parts, nrow = (int)vx.rows_pad;
+    auto fv = [&](auto kern) {
+        kern<<<ncol + nrow, 256, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n, n, vw2.scratch,
+                                          vw2.rows_pad, col_blocks, ncol, nrow, 127.f);
+    };
+    auto p2 = [&]() { CK(launch_pack_cols_pass2(W, n, k, n, 127.f, vw, s0)); };
     struct V { const char *name; std::function<void()> f; };
     std::vector<V> vs = {{"fused_pass1", fused}, {"rows_only", rows_only}, {"colmax_only", colmax_only},
                          {"pass2_tpb4", [&] { CK(launch_pack_cols_pass2(W, n, k, n, 127.f, vw, s0)); }},
@@ -50,13 +70,29 @@ int main(int argc, char **argv) {
                          {"pass2_tpb16", [&] { pass2<16>(W, k, n, vw2, s0); }},
                          {"pass2_tpb32", [&] { pass2<32>(W, k, n, vw2, s0); }},
                          {"split_r_c", [&] { rows_only(); colmax_only(); }},
-                         {"split_c_r", [&] { colmax_only(); rows_only(); }}};
+                         {"split_c_r", [&] { colmax_only(); rows_only(); }},
+                         {"call_lib", [&] { fused(); p2(); }},
+                         {"call_u8", [&] { fv(fused_var<8, false>); p2(); }},
+                         {"call_u16", [&] { fv(fused_var<16, false>); p2(); }},
+                         {"call_u4", [&] { fv(fused_var<4, false>); p2(); }},
+                         {"call_u16_xf", [&] { fv(fused_var<16, true>); p2(); }},
+                         {"call_u8_xf", [&] { fv(fused_var<8, true>); p2(); }}};
     for (int v = 4; v < 8; ++v) {
         sync_partials(); CK(hipMemsetAsync(vw2.q, 0x5a, vw2.rows_pad * vw2.k_pad, s0));
         vs[v].f(); CK(hipStreamSynchronize(s0));
         std::vector<char> a(vw.rows_pad * vw.k_pad), b(a.size());
         CK(hipMemcpy(a.data(), vw.q, a.size(), hipMemcpyDeviceToHost)); CK(hipMemcpy(b.data(), vw2.q, b.size(), hipMemcpyDeviceToHost));
         printf("%-12s q %s\n", vs[v].name, memcmp(a.data(), b.data(), a.size()) ? "DIFF" : "same");
+    }
+    {   // the pass-1 variants' partials against the library's
+        auto chk = [&](const char *nm, auto kern) {
+            CK(hipMemsetAsync(vw2.scratch, 0x5a, part_bytes, s0)); fv(kern); CK(hipStreamSynchronize(s0));
+            std::vector<char> a(part_bytes), b(part_bytes);
+            CK(hipMemcpy(a.data(), vw.scratch, part_bytes, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(b.data(), vw2.scratch, part_bytes, hipMemcpyDeviceToHost));
+            printf("%-12s partials %s\n", nm, memcmp(a.data(), b.data(), part_bytes) ? "DIFF" : "same");
+        };
+        chk("u16", fused_var<16, false>); chk("u4", fused_var<4, false>); chk("u16_xf", fused_var<16, true>);
     }
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     std::vector<std::vector<float>> t(vs.size());
@@ -69,7 +105,8 @@ int main(int argc, char **argv) {
             float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t[i].push_back(ms * 1000 / reps);
         }
     const double xb = 4.0 * m * k + (double)m * k, wb1 = 4.0 * k * n, wb2 = 4.0 * k * n + (double)k * n;
-    const double bytes[10] = {xb + wb1, xb, wb1, wb2, wb2, wb2, wb2, wb2, xb + wb1, xb + wb1};
+    const double cb = xb + wb1 + wb2;
+    const double bytes[16] = {xb + wb1, xb, wb1, wb2, wb2, wb2, wb2, wb2, xb + wb1, xb + wb1, cb, cb, cb, cb, cb, cb};
     for (size_t i = 0; i < vs.size(); ++i) {
         auto v = t[i]; std::sort(v.begin(), v.end());
         printf("%-12s median %8.2f us  (%.2f TB/s)\n", vs[i].name, v[v.size() / 2], bytes[i] / (v[v.size() / 2] * 1e-6) / 1e12);
