@@ -329,7 +329,7 @@ __device__ __forceinline__ void colmax_body(int cb, int part, const float *__res
         const int64_t c = c0 + lane * 4;
         if (c < cols) {
             const float *base = src + c;
-#pragma unroll(kUnroll)
+#pragma unroll kUnroll
             for (int64_t r = r0; r < r1; ++r) {
                 const float4 x = *reinterpret_cast<const float4 *>(base + r * sh);
                 p0 = cand_max(p0, x.x);
@@ -612,6 +612,151 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Single pass for WIDE W (n >= 16384, 2048 < K <= 4096): 32-column strips, so each row segment of W a
+// block reads is 128 B -- the 16-column pass's 64-B segments stream at 3.8-3.9 TB/s at n = 16384 / 32768
+// (row strides of 64 / 128 KiB).  A 32-column strip of 4096 rows is 512 KiB: one 1024-thread block per
+// CU holds rows < 3072 in registers (24 float4 per thread, 96 VGPRs) and rows 3072..4095 in LDS (128 KiB
+// through buffer_load ... lds; a lane's slot is the one its own DMA writes, so it reads its rows back
+// conflict-free after its own vmcnt, no barrier).  Thread t: c8 = t & 7 (columns n0 + 4*c8 .. +3), rq =
+// t >> 3: rows 4*rq + e + 512*i -- one wave instruction reads 8 rows x 128 B.  lab/pack32_lab.hip
+// (2048 x n x 4096, µs, 16-column vs 32-column): n = 16384 98.0 -> 85.2, 32768 182.7 -> 162.6, 24576
+// 125.3 -> 119.2 (1024 rows: 93.2 -> 87.7); narrower W stays on the 16- / 8-column passes (12288: 59.2 vs
+// 62.4, 8192: 43.1 vs 44.5, 4096: 28.7 vs 34.4; 20480 106.8 vs 110.3; K = 2048 37.7 vs 38.9).
+constexpr int kW32Cols = 32;
+constexpr int kW32RegI = 6;                      // row blocks of 512 held in registers
+constexpr int kW32LdsI = 8 - kW32RegI;           // row blocks of 512 held in LDS
+constexpr int kW32LdsBytes = kW32LdsI * 4 * 16 * 1024;  // [i][e][wave] x 1 KiB
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
+                                                    float range, float *__restrict__ scale, int8_t *__restrict__ q,
+                                                    int64_t k_pad, uint8_t *lds, float *red) {
+    typedef int v4i_t __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int c8 = t & 7, rq = t >> 3;  // columns n0 + 4*c8 .. +3; rows 4*rq + e + 512*i
+    const int64_t n0 = (int64_t)strip * kW32Cols;
+    const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kW32Cols) * 4));
+    const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c8) * 4);
+    // LDS part first (rows 512*kW32RegI ..): lane-linear DMA slots
+#pragma unroll
+    for (int i = 0; i < kW32LdsI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                src, (lds_void *)(lds + ((i * 4 + e) * 16 + wv) * 1024), 16,
+                (int)(vrow + (uint32_t)((e + 512 * (i + kW32RegI)) * wsh * 4)), 0, 0, 0);
+    float4 v[kW32RegI][4];
+#pragma unroll
+    for (int i = 0; i < kW32RegI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 512 * i) * wsh * 4), 0, 0);
+            v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
+        }
+    float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < kW32RegI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 512 * i;
+            if (r >= 1 && r < k) {
+                p0 = cand_max(p0, v[i][e].x);
+                p1 = cand_max(p1, v[i][e].y);
+                p2 = cand_max(p2, v[i][e].z);
+                p3 = cand_max(p3, v[i][e].w);
+            }
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA slots have landed
+    const float4 *ls = reinterpret_cast<const float4 *>(lds) + wv * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < kW32LdsI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * rq + e + 512 * (i + kW32RegI);
+            if (r < k) {
+                const float4 x = ls[(i * 4 + e) * 16 * 64];
+                p0 = cand_max(p0, x.x);
+                p1 = cand_max(p1, x.y);
+                p2 = cand_max(p2, x.z);
+                p3 = cand_max(p3, x.w);
+            }
+        }
+    // over the 8 lanes of the wave with the same c8 (lane bits 3..5), then over the 16 waves
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1) {
+        p0 = fmaxf(p0, __shfl_xor(p0, off, 64));
+        p1 = fmaxf(p1, __shfl_xor(p1, off, 64));
+        p2 = fmaxf(p2, __shfl_xor(p2, off, 64));
+        p3 = fmaxf(p3, __shfl_xor(p3, off, 64));
+    }
+    if (lane < 8) {
+        red[wv * 32 + 4 * lane + 0] = p0;
+        red[wv * 32 + 4 * lane + 1] = p1;
+        red[wv * 32 + 4 * lane + 2] = p2;
+        red[wv * 32 + 4 * lane + 3] = p3;
+    }
+    __syncthreads();
+    float *s_sh = red + 16 * 32;
+    if (t < kW32Cols) {
+        float pm = red[t];
+#pragma unroll
+        for (int ww = 1; ww < 16; ++ww) pm = fmaxf(pm, red[ww * 32 + t]);  // -inf or >= +0: exact
+        const float cw = absmax_finish(w[n0 + t], pm);                    // seed = W[0, j]
+        s_sh[t] = inv_divide(range, cw);
+        scale[n0 + t] = cw;
+    }
+    __syncthreads();
+    const float s0 = s_sh[4 * c8 + 0], s1 = s_sh[4 * c8 + 1], s2 = s_sh[4 * c8 + 2], s3 = s_sh[4 * c8 + 3];
+    const auto dst = buf_rsrc(q + n0 * k_pad, (uint32_t)(kW32Cols * k_pad));
+    const uint32_t vq = (uint32_t)(4 * c8 * k_pad + 4 * rq);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r0 = 4 * rq + 512 * i;
+        if (r0 >= k_pad) continue;
+        float4 x4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x4[e] = i < kW32RegI ? v[i < kW32RegI ? i : 0][e] : ls[((i - kW32RegI) * 4 + e) * 16 * 64];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            int qe[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = cc == 0 ? x4[e].x : cc == 1 ? x4[e].y : cc == 2 ? x4[e].z : x4[e].w;
+                const float sc = cc == 0 ? s0 : cc == 1 ? s1 : cc == 2 ? s2 : s3;
+                qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
+            }
+            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst, vq,
+                                                  (uint32_t)(cc * k_pad + 512 * i), 0);
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
+    const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
+    int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
+    int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_w[kW32LdsBytes];
+    __shared__ float red[16 * 32 + 32];
+    zero_words_block0(zero_words, nzero);
+    const int bid = blockIdx.x;
+    const int npad = (int)((w_rows_pad - n) / kW32Cols);
+    if (bid < nstrips) {
+        const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
+        const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        pack_w_strip32_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
+    } else if (bid < nstrips + npad) {
+        const int64_t n0 = n + (int64_t)(bid - nstrips) * kW32Cols;
+        for (int64_t i = threadIdx.x; i < (int64_t)kW32Cols * k_pad / 16; i += 1024)
+            reinterpret_cast<uint4 *>(w_q + n0 * k_pad)[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x < kW32Cols) w_scale[n0 + threadIdx.x] = 0.0f;
+    } else {
+        const int64_t xb = bid - nstrips - npad;
+        pack_rows_vec_body<16>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Single pass at TWO blocks per CU (K <= 4096, n % 8 == 0): 512-thread blocks with the same 16 float4
 // per thread, so a block fits in 88 VGPRs (5 waves/SIMD) and a second block on the CU streams its
 // loads while the first reduces, quantizes and stores (the 1024-thread single pass leaves the CU's HBM
@@ -852,7 +997,19 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
     if (k < 1 || k > kWsMaxK || !rows_vec_ok(x, xsh, 1, m) || !cols_vec_ok(w, wsh, n)) return hipErrorNotSupported;
     const bool can8 = n % kWs8Cols == 0 && ((int64_t)k * wsh + kWs8Cols) * 4 < ((int64_t)1 << 31);
     const bool can16 = n % kWsCols == 0;
-    if (kind == 0) kind = (can8 && n <= 8192 && k > 1024) || !can16 ? 8 : 16;
+    const bool can32 = n % kW32Cols == 0 && ((int64_t)k * wsh + kW32Cols) * 4 < ((int64_t)1 << 31);
+    if (kind == 0) kind = (can32 && n >= 16384 && k > 2048) ? 32 : (can8 && n <= 8192 && k > 1024) || !can16 ? 8 : 16;
+    if (kind == 32) {
+        if (!can32) return hipErrorNotSupported;
+        const int nstrips = n / kW32Cols;
+        const int npad = (int)((outw.rows_pad - n) / kW32Cols);
+        const int nx = (int)(outx.rows_pad / 16);
+        pack_single_pass32_kernel<<<nstrips + npad + nx, 1024, 0, stream>>>(x, xsh, m, k, outx.scale, outx.q,
+                                                                            outx.rows_pad, outx.k_pad, w, wsh, n,
+                                                                            outw.scale, outw.q, outw.rows_pad, nstrips,
+                                                                            range, zero_words, nzero);
+        return hipGetLastError();
+    }
     if (kind == 8) {
         if (!can8) return hipErrorNotSupported;
         const int nstrips = n / kWs8Cols;

@@ -1,0 +1,71 @@
+// pack32_lab.hip -- development harness (not part of the library): the single pass's strip widths (8, 16
+// and 32 columns: pack_single_pass8 / pack_single_pass / pack_single_pass32 in csrc/pack.hip) at one shape,
+// the 32-column pass bit-compared with the 16-column one, all timed back to back.
+// Build: make -C .. pack32lab   Run: build/pack32_lab [m n k reps]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+#include <functional>
+#include <cstring>
+
+#include "../csrc/pack.hip"
+
+using namespace qgemm;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static void launch32(const float *X, int m, int k, PackedView vx, const float *W, int n, PackedView vw, hipStream_t s) {
+    CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s, 32));
+}
+
+int main(int argc, char **argv) {
+    int m = argc > 1 ? atoi(argv[1]) : 2048, n = argc > 2 ? atoi(argv[2]) : 16384, k = argc > 3 ? atoi(argv[3]) : 4096;
+    int reps = argc > 4 ? atoi(argv[4]) : 10;
+    if (n % kW32Cols || k > 4096 || k % 4) { printf("shape outside the 32-column pass\n"); return 1; }
+    float *X, *W; void *PX, *PW, *PX2, *PW2;
+    CK(hipMalloc(&X, (size_t)m * k * 4)); CK(hipMalloc(&W, (size_t)k * n * 4));
+    CK(hipMalloc(&PX, packed_bytes(m, k))); CK(hipMalloc(&PW, packed_bytes(n, k)));
+    CK(hipMalloc(&PX2, packed_bytes(m, k))); CK(hipMalloc(&PW2, packed_bytes(n, k)));
+    CK(launch_fill_uniform(X, (int64_t)m * k, 11, -1.f, 1.f, nullptr));
+    CK(launch_fill_uniform(W, (int64_t)k * n, 12, -1.f, 1.f, nullptr));
+    PackedView vx = packed_view(PX, m, k), vw = packed_view(PW, n, k), vx2 = packed_view(PX2, m, k),
+               vw2 = packed_view(PW2, n, k);
+    hipStream_t s0; CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+    CK(hipMemset(PX2, 0x5a, packed_bytes(m, k))); CK(hipMemset(PW2, 0x5a, packed_bytes(n, k)));
+    CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s0, n % 16 ? 8 : 16));
+    launch32(X, m, k, vx2, W, n, vw2, s0);
+    CK(hipStreamSynchronize(s0));
+    CK(hipGetLastError());
+    auto cmp = [&](const void *a, const void *b, size_t bytes, const char *what) {
+        std::vector<char> ha(bytes), hb(bytes);
+        CK(hipMemcpy(ha.data(), a, bytes, hipMemcpyDeviceToHost)); CK(hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost));
+        size_t diff = 0;
+        for (size_t i = 0; i < bytes; ++i) diff += ha[i] != hb[i];
+        printf("%-10s %s (%zu of %zu bytes differ)\n", what, diff ? "DIFF" : "same", diff, bytes);
+    };
+    cmp(vw.scale, vw2.scale, vw.rows_pad * 4, "w scale");
+    cmp(vw.q, vw2.q, vw.rows_pad * vw.k_pad, "w q");
+    cmp(vx.scale, vx2.scale, vx.rows_pad * 4, "x scale");
+    cmp(vx.q, vx2.q, vx.rows_pad * vx.k_pad, "x q");
+    struct V { const char *name; std::function<void()> f; };
+    std::vector<V> vs = {{"strip16", [&] { CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s0, n % 16 ? 8 : 16)); }},
+                         {"strip8", [&] { CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s0, 8)); }},
+                         {"strip32", [&] { launch32(X, m, k, vx2, W, n, vw2, s0); }}};
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> tm(vs.size());
+    for (int r = 0; r < 5; ++r)
+        for (size_t i = 0; i < vs.size(); ++i) {
+            vs[i].f(); vs[i].f();
+            CK(hipEventRecord(e0, s0));
+            for (int j = 0; j < reps; ++j) vs[i].f();
+            CK(hipEventRecord(e1, s0)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); tm[i].push_back(ms * 1000 / reps);
+        }
+    const double bytes = 4.0 * m * k + (double)m * k + 4.0 * k * n + (double)k * n;
+    for (size_t i = 0; i < vs.size(); ++i) {
+        auto v = tm[i]; std::sort(v.begin(), v.end());
+        printf("%-10s median %8.2f us  min %8.2f  (%.2f TB/s)\n", vs[i].name, v[v.size() / 2], v[0],
+               bytes / (v[v.size() / 2] * 1e-6) / 1e12);
+    }
+    return 0;
+}
