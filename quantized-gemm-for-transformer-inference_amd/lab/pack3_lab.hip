@@ -14,6 +14,99 @@
 using namespace qgemm;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
+namespace qgemm {
+// Experiment (round 2, not in the library): pack_cols pass 2, wide form: a block = 256 input columns (1-KiB row segments of W; the 64-column
+// tiles above read 256-B segments) x kTPB k-tiles of 32 rows.  Each tile's quantized dwords go to an LDS
+// image of the block's 256 packed rows x kTPB*32 bytes, written out once at the end as 256-B runs per
+// packed row.  Thread t: col4 = t & 63 (columns n0 + 4*col4 .. +3), rg = t >> 6: rows k0 + 4*rg + 16*h + i.
+constexpr int kTcW = 256;
+constexpr int kTkW = 32;
+template <int kTPB>
+__global__ __launch_bounds__(256) void pack_cols_wide_kernel(const float *__restrict__ src, int64_t sh, int len,
+                                                             int cols, float range, const uint32_t *__restrict__ partial,
+                                                             int64_t parts, int64_t rows_pad, float *__restrict__ scale,
+                                                             int8_t *__restrict__ q, int64_t k_pad) {
+    constexpr int kRow = kTPB * kTkW + 4;  // LDS image row stride (bytes): odd dword count
+    __shared__ __attribute__((aligned(16))) uint8_t img[kTcW * kRow];
+    __shared__ float s_sh[kTcW];
+    const int t = threadIdx.x;
+    const int64_t n0 = (int64_t)blockIdx.x * kTcW;
+    const int64_t nkt = k_pad / kTkW;
+    const int64_t kt0 = (int64_t)blockIdx.y * kTPB;
+    const int64_t kt1 = min(nkt, kt0 + kTPB);
+    const int col4 = t & 63, rg = t >> 6;
+    const int64_t c = n0 + 4 * col4;
+    auto load = [&](float4 (&x)[2][4], int64_t k0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t kk = k0 + 4 * rg + 16 * h + i;
+                x[h][i] = (kk < len && c < cols) ? *reinterpret_cast<const float4 *>(src + kk * sh + c)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+    };
+    float4 x[2][4], xn[2][4];
+    load(x, kt0 * kTkW);
+    {
+        const int64_t j = n0 + t;
+        float cx = 0.0f, s = 0.0f;
+        if (j < cols) {
+            float p = -INFINITY;
+#pragma unroll 16
+            for (int64_t part = 0; part < parts; ++part) p = fmaxf(p, dec_partial(partial[part * rows_pad + j]));
+            cx = absmax_finish(src[j], p);  // seed = row 0 (op_reduction.cuh:105)
+            s = inv_divide(range, cx);
+        }
+        s_sh[t] = s;
+        if (blockIdx.y == 0) scale[j] = cx;
+    }
+    __syncthreads();
+    const float s0 = s_sh[4 * col4 + 0], s1 = s_sh[4 * col4 + 1], s2 = s_sh[4 * col4 + 2], s3 = s_sh[4 * col4 + 3];
+    for (int64_t kt = kt0; kt < kt1; ++kt) {
+        const int64_t k0 = kt * kTkW;
+        if (kt + 1 < kt1) load(xn, k0 + kTkW);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int qv[4][4];  // [row i][col e]
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool in = k0 + 4 * rg + 16 * h + i < len;
+                qv[i][0] = (in && c + 0 < cols) ? quant_i8(x[h][i].x, s0) : 0;
+                qv[i][1] = (in && c + 1 < cols) ? quant_i8(x[h][i].y, s1) : 0;
+                qv[i][2] = (in && c + 2 < cols) ? quant_i8(x[h][i].z, s2) : 0;
+                qv[i][3] = (in && c + 3 < cols) ? quant_i8(x[h][i].w, s3) : 0;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                *reinterpret_cast<uint32_t *>(img + (4 * col4 + e) * kRow + (kt - kt0) * kTkW + 4 * rg + 16 * h) =
+                    pack4(qv[0][e], qv[1][e], qv[2][e], qv[3][e]);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[h][i] = xn[h][i];
+    }
+    __syncthreads();
+    // write-out: packed row r's (kt1 - kt0) * 32 bytes as 16-B pieces; a wave covers 4 rows x 256 B
+    const int chunks = (int)(kt1 - kt0) * (kTkW / 16);
+    for (int u = t; u < kTcW * (kTPB * kTkW / 16); u += 256) {
+        const int r = u / (kTPB * kTkW / 16), ch = u % (kTPB * kTkW / 16);
+        if (ch >= chunks) continue;
+        const uint32_t *lp = reinterpret_cast<const uint32_t *>(img + r * kRow + ch * 16);
+        *reinterpret_cast<uint4 *>(q + (n0 + r) * k_pad + kt0 * kTkW + ch * 16) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+    }
+}
+
+}  // namespace qgemm
+
+template <int TPB>
+static void pass2w(const float *W, int k, int n, PackedView vw, hipStream_t s) {
+    const dim3 g2((unsigned)(vw.rows_pad / kTcW), (unsigned)((vw.k_pad / kTkW + TPB - 1) / TPB));
+    pack_cols_wide_kernel<TPB><<<g2, 256, 0, s>>>(W, n, k, n, 127.f, vw.scratch, vw.parts, vw.rows_pad, vw.scale, vw.q,
+                                                  vw.k_pad);
+}
+
 template <int TPB>
 static void pass2(const float *W, int k, int n, PackedView vw, hipStream_t s) {
     const dim3 g2((unsigned)(vw.rows_pad / kTc), (unsigned)((vw.k_pad / kTk + TPB - 1) / TPB));
@@ -69,6 +162,9 @@ int main(int argc, char **argv) {
                          {"pass2_tpb8", [&] { pass2<8>(W, k, n, vw2, s0); }},
                          {"pass2_tpb16", [&] { pass2<16>(W, k, n, vw2, s0); }},
                          {"pass2_tpb32", [&] { pass2<32>(W, k, n, vw2, s0); }},
+                         {"pass2w_8", [&] { pass2w<8>(W, k, n, vw2, s0); }},
+                         {"pass2w_4", [&] { pass2w<4>(W, k, n, vw2, s0); }},
+                         {"pass2w_16", [&] { pass2w<16>(W, k, n, vw2, s0); }},
                          {"split_r_c", [&] { rows_only(); colmax_only(); }},
                          {"split_c_r", [&] { colmax_only(); rows_only(); }},
                          {"call_lib", [&] { fused(); p2(); }},
@@ -77,7 +173,7 @@ int main(int argc, char **argv) {
                          {"call_u4", [&] { fv(fused_var<4, false>); p2(); }},
                          {"call_u16_xf", [&] { fv(fused_var<16, true>); p2(); }},
                          {"call_u8_xf", [&] { fv(fused_var<8, true>); p2(); }}};
-    for (int v = 4; v < 8; ++v) {
+    for (int v = 4; v < 11; ++v) {
         sync_partials(); CK(hipMemsetAsync(vw2.q, 0x5a, vw2.rows_pad * vw2.k_pad, s0));
         vs[v].f(); CK(hipStreamSynchronize(s0));
         std::vector<char> a(vw.rows_pad * vw.k_pad), b(a.size());
@@ -106,7 +202,8 @@ int main(int argc, char **argv) {
         }
     const double xb = 4.0 * m * k + (double)m * k, wb1 = 4.0 * k * n, wb2 = 4.0 * k * n + (double)k * n;
     const double cb = xb + wb1 + wb2;
-    const double bytes[16] = {xb + wb1, xb, wb1, wb2, wb2, wb2, wb2, wb2, xb + wb1, xb + wb1, cb, cb, cb, cb, cb, cb};
+    const double bytes[19] = {xb + wb1, xb, wb1, wb2, wb2, wb2, wb2, wb2, wb2, wb2, wb2, xb + wb1, xb + wb1,
+                              cb, cb, cb, cb, cb, cb};
     for (size_t i = 0; i < vs.size(); ++i) {
         auto v = t[i]; std::sort(v.begin(), v.end());
         printf("%-12s median %8.2f us  (%.2f TB/s)\n", vs[i].name, v[v.size() / 2], bytes[i] / (v[v.size() / 2] * 1e-6) / 1e12);
