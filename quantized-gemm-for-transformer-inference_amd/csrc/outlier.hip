@@ -69,47 +69,59 @@ __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restr
 }
 
 // bits[w] = OR of the chunk masks, rank[w] = set bits below word w, idx[1 + ...] = the outlier columns in
-// ascending order, idx[0] = their count.  One block.
+// ascending order, idx[0] = their count.  One block; P adjacent threads share a word (each ORs every P-th
+// chunk, one round of loads in flight, then a shuffle-OR), 1024 / P words per pass; the ranks by a wave
+// scan + a scan of the 16 wave sums.
+template <int P>
 __global__ __launch_bounds__(1024) void outlier_index_kernel(const uint32_t *__restrict__ partial, int nchunks,
                                                              int nwords, uint32_t *__restrict__ bits,
                                                              int *__restrict__ rank, int *__restrict__ idx) {
-    __shared__ int scan[1024];
+    __shared__ int wsum[16];
     __shared__ int base;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int s = tid % P;
     if (tid == 0) base = 0;
     __syncthreads();
-    for (int w0 = 0; w0 < nwords; w0 += 1024) {
-        const int w = w0 + tid;
+    for (int w0 = 0; w0 < nwords; w0 += 1024 / P) {
+        const int w = w0 + tid / P;
         uint32_t word = 0;
         if (w < nwords) {
-            int ch = 0;
-            for (; ch + 16 <= nchunks; ch += 16) {  // 16 loads in flight
-                uint32_t u[16];
+            int ch = s;
+            for (; ch + 7 * P < nchunks; ch += 8 * P) {  // 8 loads in flight per thread
+                uint32_t u[8];
 #pragma unroll
-                for (int e = 0; e < 16; ++e) u[e] = partial[(int64_t)(ch + e) * nwords + w];
+                for (int e = 0; e < 8; ++e) u[e] = partial[(int64_t)(ch + e * P) * nwords + w];
 #pragma unroll
-                for (int e = 0; e < 16; ++e) word |= u[e];
+                for (int e = 0; e < 8; ++e) word |= u[e];
             }
-            for (; ch < nchunks; ++ch) word |= partial[(int64_t)ch * nwords + w];
+            for (; ch < nchunks; ch += P) word |= partial[(int64_t)ch * nwords + w];
         }
-        const int pc = __popc(word);
-        scan[tid] = pc;
+#pragma unroll
+        for (int off = 1; off < P; off <<= 1) word |= (uint32_t)__shfl_xor((int)word, off, 64);
+        const int pc = (s == 0 && w < nwords) ? __popc(word) : 0;
+        int x = pc;  // inclusive scan over the block in thread order (= word order)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(x, off, 64);
+            if (lane >= off) x += v;
+        }
+        if (lane == 63) wsum[wave] = x;
         __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-            const int v = tid >= off ? scan[tid - off] : 0;
-            __syncthreads();
-            scan[tid] += v;
-            __syncthreads();
-        }
-        const int below = base + scan[tid] - pc;
-        if (w < nwords) {
+        int before = base;
+        for (int j = 0; j < wave; ++j) before += wsum[j];
+        const int below = before + x - pc;
+        if (s == 0 && w < nwords) {
             bits[w] = word;
             rank[w] = below;
             int j = 0;
             for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
         }
         __syncthreads();
-        if (tid == 1023) base += scan[1023];
+        if (tid == 0) {
+            int tot = 0;
+            for (int j = 0; j < 16; ++j) tot += wsum[j];
+            base += tot;
+        }
         __syncthreads();
     }
     if (tid == 0) idx[0] = base;
@@ -188,7 +200,12 @@ hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, cons
     const bool vec = (k % 4 == 0) && (xsh % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
     if (vec) outlier_flags_kernel<true><<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords);
     else outlier_flags_kernel<false><<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords);
-    outlier_index_kernel<<<1, 1024, 0, s>>>(v.partial, v.nchunks, v.nwords, v.bits, v.rank, v.idx);
+    const int nw = v.nwords;
+    if (nw <= 64) outlier_index_kernel<16><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
+    else if (nw <= 128) outlier_index_kernel<8><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
+    else if (nw <= 256) outlier_index_kernel<4><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
+    else if (nw <= 512) outlier_index_kernel<2><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
+    else outlier_index_kernel<1><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
     return hipGetLastError();
 }
 
