@@ -152,10 +152,13 @@ def test_split_k_poisoned_caller_workspace(qg, oracle, device, M, N, K, layout):
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 8196, 300), (33, 12288, 4096), (128, 16384, 1000), (5, 9000, 2049),
-                                   (300, 8704, 513)])
+                                   (300, 8704, 513), (300, 16384, 3001), (64, 16384, 2500), (257, 32768, 4096),
+                                   (96, 16416, 3073), (1, 16384, 4096)])
 def test_wide_w_pack_poisoned_workspace(qg, oracle, device, M, N, K):
     """Wide W (n > 8192, 256 < K <= 4096, the FFN-up shape class) on a workspace full of 0xFF, twice:
-    16-column strips, n % 16 != 0 (8-column strips), K not a multiple of 128."""
+    16-column strips, n % 16 != 0 (8-column strips), K not a multiple of 128; n >= 16384 with K > 2048:
+    the 32-column pass (rows >= 3072 through LDS; K % 4 != 0, K just past the register rows, n not a
+    power of two, one row of X)."""
     X, W = oracle.inputs(M, N, K, 93)
     want = oracle.quantized_mm(X, W)
     L = qg.load()
