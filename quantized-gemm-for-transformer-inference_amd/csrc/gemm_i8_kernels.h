@@ -85,6 +85,10 @@ struct GemmArgs {
 // kEpiOutlier: the LLM.int8() decomposition's fp32 part, O = fl(O8 + fmaf chain over the outlier
 // columns in ascending k of xo[i][t] * wo[t][j]) (outlier.hip; the oracle's oracle_mm_outlier)
 enum EpiMode { kEpiNone = 0, kEpiBias = 1, kEpiBiasRelu = 2, kEpiOutlier = 3 };
+// kEpiOutlier with <= kOutlierStaged outlier columns: the tile's xo [256 rows][8] and wo [8][256 cols] are
+// staged in LDS behind the Cx / Cw slots (loads issued before the ring is released)
+constexpr int kOutlierStaged = 8;
+constexpr int kOutlierStageBytes = 2 * 256 * kOutlierStaged * 4;
 constexpr bool has_bias(int e) { return e == kEpiBias || e == kEpiBiasRelu; }
 
 constexpr int64_t kSlabInts = (int64_t)BM * BN;
@@ -304,8 +308,11 @@ __device__ __forceinline__ float epi_extra(float o, const float *sB, int jl) {
 // chain runs for 8 rows at once, 4 outlier columns per step: one load brings the 8 x 4 xo values (lane
 // 8g + tt: row g, column tt), v_readlane hands each to the wave as a scalar, one float4 of wo per column
 // serves the 8 rows.  Columns past n read wo's padding and are never stored.
+// sX [256 tile rows][8] / sW [8][256 tile cols]: the staged xo / wo values when ocnt <= kOutlierStaged
+// (nullptr otherwise); gi0 = the tile's first row.
 __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const float *T, int i0, int gj0, int c4,
-                                                      int tid, bool full) {
+                                                      int tid, bool full, const float *sX, const float *sW,
+                                                      int gi0) {
     const int ocnt = *p.ocount;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
@@ -316,6 +323,40 @@ __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const f
     for (int q0 = 0; q0 < 16; q0 += 8) {
         const int ib = i0 + wv + 8 * q0;  // rows ib + 8g, g < 8
         if (ib >= p.m) break;
+        if (sX) {  // staged: every operand from LDS (xo reads are wave-uniform: broadcast)
+            float c[8][4];
+#pragma unroll
+            for (int g = 0; g < 8; ++g) c[g][0] = c[g][1] = c[g][2] = c[g][3] = 0.0f;
+#pragma unroll
+            for (int t = 0; t < kOutlierStaged; ++t) {
+                if (t >= ocnt) break;
+                const float4 w4 = *reinterpret_cast<const float4 *>(sW + t * 256 + c4);
+#pragma unroll
+                for (int g = 0; g < 8; ++g) {
+                    const float xs = sX[(ib + 8 * g - gi0) * kOutlierStaged + t];
+                    c[g][0] = __fmaf_rn(xs, w4.x, c[g][0]);
+                    c[g][1] = __fmaf_rn(xs, w4.y, c[g][1]);
+                    c[g][2] = __fmaf_rn(xs, w4.z, c[g][2]);
+                    c[g][3] = __fmaf_rn(xs, w4.w, c[g][3]);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const int i = ib + 8 * g;
+                if (i >= p.m) break;
+                const float4 o = *reinterpret_cast<const float4 *>(T + (i - i0) * BN + c4);
+                const float vv[4] = {__fadd_rn(o.x, c[g][0]), __fadd_rn(o.y, c[g][1]), __fadd_rn(o.z, c[g][2]),
+                                     __fadd_rn(o.w, c[g][3])};
+                if (full) {
+                    *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+                }
+            }
+            continue;
+        }
         const float *xl = p.xo + (int64_t)min(ib + 8 * (lane >> 3), p.m - 1) * ocnt + (lane & 7);
         float c[8][4];
 #pragma unroll
@@ -391,11 +432,38 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
     float *sCw = sCx + BM;
     float *sB = sCw + BN;  // bias (kEpi >= 1): needs kLdsBytes + 3 KiB
     float *C = static_cast<float *>(p.C);
+    // kEpiOutlier, <= kOutlierStaged outlier columns: this tile's xo rows and wo columns are loaded here,
+    // ahead of the barrier (their latency hides under the ring drain), and parked in LDS behind Cx / Cw
+    float *sX = reinterpret_cast<float *>(lds + kLdsBytes + 2048), *sW = sX + 256 * kOutlierStaged;
+    bool staged = false;
+    float xs4[4] = {0.f, 0.f, 0.f, 0.f};
+    float4 ws4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (kEpi == kEpiOutlier && kMode != kStoreDirect) {
+        const int oc = *p.ocount;
+        staged = oc > 0 && oc <= kOutlierStaged;
+        if (staged) {
+            const int64_t r = min(gi0 + (tid >> 1), p.m - 1);  // xo: tile row tid >> 1, columns 4 (tid & 1) ..
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * (tid & 1) + e;
+                xs4[e] = c < oc ? p.xo[r * oc + c] : 0.0f;
+            }
+            const int wrow = tid >> 6;  // wo: row tid >> 6, tile columns 4 (tid & 63) ..
+            if (wrow < oc) ws4 = *reinterpret_cast<const float4 *>(p.wo + wrow * p.wo_ld + gj0 + 4 * (tid & 63));
+        }
+    }
     __syncthreads();  // every wave is done with the staging ring
     if (tid < BM) sCx[tid] = p.Cx[gi0 + tid];
     else sCw[tid - BM] = p.Cw[gj0 + tid - BM];
     if constexpr (has_bias(kEpi))
         if (tid < BN) sB[tid] = gj0 + tid < p.n ? p.bias[gj0 + tid] : 0.0f;
+    if constexpr (kEpi == kEpiOutlier && kMode != kStoreDirect) {
+        if (staged) {  // visible after the barrier that opens the first half
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sX[(tid >> 1) * kOutlierStaged + 4 * (tid & 1) + e] = xs4[e];
+            *reinterpret_cast<float4 *>(sW + (tid >> 6) * 256 + 4 * (tid & 63)) = ws4;
+        }
+    }
     if constexpr (kMode == kStoreDirect) {
         __syncthreads();
 #pragma unroll
@@ -440,7 +508,8 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
             const int c4 = (tid & 63) * 4;
             if constexpr (kEpi == kEpiOutlier) {
                 if (*p.ocount > 0) {
-                    epilogue_outlier_half(p, T, gi0 + half * 128, gj0, c4, tid, full);
+                    epilogue_outlier_half(p, T, gi0 + half * 128, gj0, c4, tid, full, staged ? sX : nullptr, sW,
+                                          gi0);
                     continue;
                 }
             }
@@ -630,7 +699,9 @@ __device__ unsigned long long g_pp_stamp[4096 * 6];
 
 // LDS bytes of the ping-pong body (staging ring + scales/bias/flag)
 template <int kEpi>
-constexpr int pp_lds_bytes() { return kLdsBytes + (has_bias(kEpi) ? 3072 : 2048); }
+constexpr int pp_lds_bytes() {
+    return kLdsBytes + (has_bias(kEpi) ? 3072 : 2048) + (kEpi == kEpiOutlier ? kOutlierStageBytes : 0);
+}
 
 // One 256 x 256 tile (k-slice `slice` of S) of the ping-pong GEMM on a 512-thread block; `lds` holds
 // pp_lds_bytes<kEpi>() bytes.  The body of gemm_i8_pp and of the fused pack+GEMM launch.
