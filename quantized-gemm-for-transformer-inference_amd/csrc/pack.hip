@@ -511,6 +511,7 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c4 = t & 3, rq = t >> 2;
     const int64_t n0 = (int64_t)strip * kWsCols;
+    const float w_seed = t < kWsCols ? w[n0 + t] : 0.0f;  // W[0, j], issued first (used after the reduction)
     float *red = reinterpret_cast<float *>(lds);                 // [16 waves][16 cols]
     float *s_sh = red + 16 * 16;                                 // [16] scales
     float4 v[4][4];                                              // [i][e]
@@ -555,7 +556,7 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
         float p = red[t];
 #pragma unroll
         for (int ww = 1; ww < 16; ++ww) p = fmaxf(p, red[ww * 16 + t]);  // -inf or >= +0: exact
-        const float cw = absmax_finish(w[n0 + t], p);                   // seed = W[0, j]
+        const float cw = absmax_finish(w_seed, p);                      // seed = W[0, j]
         s_sh[t] = inv_divide(range, cw);
         scale[n0 + t] = cw;
     }
@@ -637,6 +638,7 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c8 = t & 7, rq = t >> 3;  // columns n0 + 4*c8 .. +3; rows 4*rq + e + 512*i
     const int64_t n0 = (int64_t)strip * kW32Cols;
+    const float w_seed = t < kW32Cols ? w[n0 + t] : 0.0f;  // W[0, j], issued first (used after the reduction)
     const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kW32Cols) * 4));
     const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c8) * 4);
     // LDS part first (rows 512*kW32RegI ..): lane-linear DMA slots
@@ -703,7 +705,7 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
         float pm = red[t];
 #pragma unroll
         for (int ww = 1; ww < 16; ++ww) pm = fmaxf(pm, red[ww * 32 + t]);  // -inf or >= +0: exact
-        const float cw = absmax_finish(w[n0 + t], pm);                    // seed = W[0, j]
+        const float cw = absmax_finish(w_seed, pm);                       // seed = W[0, j]
         s_sh[t] = inv_divide(range, cw);
         scale[n0 + t] = cw;
     }
@@ -781,6 +783,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c2 = t & 1, rq = t >> 1;
     const int64_t n0 = (int64_t)strip * kWs8Cols;
+    const float w_seed = t < kWs8Cols ? w[n0 + t] : 0.0f;  // W[0, j], issued first (used after the reduction)
     const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kWs8Cols) * 4));
     const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c2) * 4);
     // mask words of this thread's rows (word (4 rq + 1024 i) >> 5 for every e) and their ranks, issued
@@ -856,7 +859,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
         float pm = red[t];
 #pragma unroll
         for (int ww = 1; ww < 8; ++ww) pm = fmaxf(pm, red[ww * 8 + t]);  // -inf or >= +0: exact
-        const float cw = absmax_finish(seed_masked ? 0.0f : w[n0 + t], pm);  // seed = W[0, j] (W'[0, j])
+        const float cw = absmax_finish(seed_masked ? 0.0f : w_seed, pm);  // seed = W[0, j] (W'[0, j])
         s_sh[t] = inv_divide(range, cw);
         scale[n0 + t] = cw;
     }
