@@ -36,9 +36,9 @@ static bool shape_ok(const PackedView &a, const PackedView &b) {
 // only for K >= 4096.  Measured (gemm_lab small mode, us, 128-tiles vs 64-tiles at the chosen S):
 // 512x3072x1024 11.8 -> 7.6, 512x1024x1024 11.1 -> 6.1, 512x4096x1024 12.2 -> 8.1,
 // 512x1024x4096 16.8 (S4) -> 10.9 (S2), 256x4096x4096 20.2 (S2) -> 13.2 (S2), 2048^3 20.7 -> 18.5;
-// split-K never helped at K = 1024.
+// split-K never helped at K = 1024.  Fewer than 256 64-tiles: 32-tiles where they fill the chip (below).
 struct GemmPlan {
-    int tile;       // 256 or 64
+    int tile;       // 256, 64 or 32
     int tiles_m, tiles_n;
     int splits;
 };
@@ -58,6 +58,15 @@ static GemmPlan gemm_plan(int m, int n, int k) {
     }
     g = GemmPlan{64, (int)(round_up(m, 64) / 64), (int)(round_up(n, 64) / 64), 1};
     tiles = (int64_t)g.tiles_m * g.tiles_n;
+    // fewer 64-tiles than CUs: 32 x 32 tiles (gemm_i8_small<32>, 4-stage ring, no split) where they give
+    // >= 512 blocks, or >= 256 at K <= 2048 (gemm_lab ... small, us, best 64-tile plan -> 32-tiles:
+    // 512x1024x1024 5.65 -> 4.79, 512x1024x4096 10.07 -> 8.67, 256x1024x1024 5.50 -> 4.08, 128x2048x2048
+    // 7.58 -> 5.96, 256x2048x4096 10.05 -> 8.66, 512x1024x2048 7.73 -> 6.07; but 64x4096x4096 11.55 -> 15.21)
+    if (tiles < 256) {
+        const GemmPlan g32{32, (int)(round_up(m, 32) / 32), (int)(round_up(n, 32) / 32), 1};
+        const int64_t tiles32 = (int64_t)g32.tiles_m * g32.tiles_n;
+        if (tiles32 >= 512 || (tiles32 >= 256 && k <= 2048)) return g32;
+    }
     int sp = tiles >= 512 ? 1 : (int)(512 / tiles);
     sp = sp < nk / 16 ? sp : nk / 16;
     sp = sp < 4 ? sp : 4;
@@ -145,6 +154,10 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
         }
     }
     const dim3 grid((unsigned)(tiles * p.splits));
+    if (g.tile == 32) {
+        if (!bias) return launch_small<32, kEpiNone, 4>(p, grid, stream);
+        return relu ? launch_small<32, kEpiBiasRelu, 4>(p, grid, stream) : launch_small<32, kEpiBias, 4>(p, grid, stream);
+    }
     if (g.tile == 64) {
         // at most two 64-tiles per CU: a 3-stage ring (two k-steps in flight, three blocks per CU); more
         // tiles: the 2-stage ring, four blocks per CU (gemm_lab ... small, us: 512x1024x1024 6.10 -> 5.67,

@@ -218,6 +218,8 @@ int main(int argc, char **argv) {
             {"t64d4_S1", gemm_i8_small<64, 0, 4>, 64, 1}, {"t64d4_S2", gemm_i8_small<64, 0, 4>, 64, 2},
             {"t64d4_S4", gemm_i8_small<64, 0, 4>, 64, 4}, {"t64d6_S1", gemm_i8_small<64, 0, 6>, 64, 1},
             {"t64d8_S1", gemm_i8_small<64, 0, 8>, 64, 1}, {"t64d8_S2", gemm_i8_small<64, 0, 8>, 64, 2},
+            {"t32d2_S1", gemm_i8_small<32>, 32, 1}, {"t32d3_S1", gemm_i8_small<32, 0, 3>, 32, 1},
+            {"t32d4_S1", gemm_i8_small<32, 0, 4>, 32, 1},
         };
         auto args = [&](const SV &v, float *out) {
             GemmArgs q = p; q.C = out; q.splits = v.S; q.slabs = slabs; q.tickets = tick; q.reset_tickets = 1;

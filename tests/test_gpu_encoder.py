@@ -54,7 +54,10 @@ def test_add_layernorm_rows_misaligned_rows(qg, oracle, device):
 
 @pytest.mark.parametrize("M,N,K,bias,relu", [(100, 260, 300, True, True), (100, 260, 300, True, False),
                                              (100, 260, 300, False, False), (512, 1024, 1024, True, True),
-                                             (512, 4096, 1024, True, False)])
+                                             (512, 4096, 1024, True, False),
+                                             # 32 x 32 tiles (fewer 64-tiles than CUs): K = 4096, ragged M / N
+                                             (512, 1024, 4096, True, False), (300, 1000, 2048, True, True),
+                                             (250, 1030, 1024, False, False)])
 def test_linear_fused_bias_relu_bit_exact(qg, oracle, device, M, N, K, bias, relu):
     X, W = oracle.inputs(M, N, K, 91)
     b = oracle.uniform((N,), 92) if bias else None
