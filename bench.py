@@ -220,6 +220,39 @@ def ctypes_count(L, K, ws):
     return c.value
 
 
+def share_comm_id(rank, distributed, make_id, nbytes):
+    """Rank 0 draws the communicator id (qgemm_comm_unique_id); every rank receives it over the
+    torch.distributed group (broadcast_object_list).  Host-side orchestration of c4_node, tested on
+    gloo (tests/test_distributed.py)."""
+    uid = make_id() if rank == 0 else bytes(nbytes)
+    if distributed:
+        import torch.distributed as dist
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    return uid
+
+
+def node_phase_times(reps, warm, distributed, run_step, dev):
+    """`warm` untimed then `reps` timed whole-node steps: barrier, run_step() -> (compute_ms, gather_ms) on this
+    rank, then the MAX over ranks of each phase (all_reduce); returns the timed steps' two lists.  Host-side
+    orchestration of c4_node, tested on gloo with a stub step (tests/test_distributed.py)."""
+    import torch
+    comp, gath = [], []
+    for it in range(warm + reps):
+        if distributed:
+            import torch.distributed as dist
+            dist.barrier()
+        c, g = run_step()
+        t = torch.tensor([c, g], device=dev, dtype=torch.float64)
+        if distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if it >= warm:
+            comp.append(float(t[0]))
+            gath.append(float(t[1]))
+    return comp, gath
+
+
 def c4_node(args, qg, dev, world, rank, distributed):
     """BASELINE configs[3] as a whole-node figure: the global M = 65536 x 4096 x 4096 problem with M sharded
     over the `world` ranks (op_mm_quantize_shard: per-rank pointer offsets into the full A and C), then the
@@ -234,18 +267,11 @@ def c4_node(args, qg, dev, world, rank, distributed):
     A = qg.fill_uniform(torch.empty((Mg, K), device=dev), seed=2 * 7)  # the same A on every rank
     B = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 7 + 1)
     C = torch.empty((Mg, N), device=dev)
-    uid = qg.Comm.unique_id() if rank == 0 else bytes(qg.COMM_ID_BYTES)
-    if distributed:
-        box = [uid]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
+    uid = share_comm_id(rank, distributed, qg.Comm.unique_id, qg.COMM_ID_BYTES)
     comm = qg.Comm(world, rank, uid)
     hip = HipEvents(3)
-    comp, gath = [], []
     try:
-        for it in range(2 + args.node_reps):
-            if distributed:
-                dist.barrier()
+        def one_step():
             torch.cuda.synchronize(dev)
             s = qg._stream(dev)
             hip.hip.hipEventRecord(hip.ev[0], s)
@@ -253,13 +279,9 @@ def c4_node(args, qg, dev, world, rank, distributed):
             hip.hip.hipEventRecord(hip.ev[1], s)
             comm.allgather_rows(C)
             hip.hip.hipEventRecord(hip.ev[2], s)
-            t = torch.tensor([hip.elapsed_ms(hip.ev[0], hip.ev[1]), hip.elapsed_ms(hip.ev[1], hip.ev[2])],
-                             device=dev, dtype=torch.float64)
-            if distributed:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            if it >= 2:
-                comp.append(float(t[0]))
-                gath.append(float(t[1]))
+            return hip.elapsed_ms(hip.ev[0], hip.ev[1]), hip.elapsed_ms(hip.ev[1], hip.ev[2])
+
+        comp, gath = node_phase_times(args.node_reps, 2, distributed, one_step, dev)
         # every rank now holds the whole C: check one row of every shard against this rank's own call
         m0, rows = qg.shard_rows(Mg, world, rank)
         probe = [qg.shard_rows(Mg, world, r)[0] for r in range(world)]
@@ -419,7 +441,7 @@ def main():
             "traffic_unit": "bytes per launch (HBM + Infinity Cache fill, FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
             "alg_bytes": M * K + N * K + 4 * M * N + 4 * (M + N),
-            "kernel": "gemm_i8_pp<1> (int8 16x16x64 MFMA GEMM, ping-pong schedule, fused dequant epilogue"
+            "kernel": "gemm_i8_pp<2> (int8 16x16x64 MFMA GEMM, ping-pong schedule, fused dequant epilogue"
                       + (" + outlier fp32 chain)" if outlier else ")"),
             "ceiling_measured": {
                 "value": PRACTICAL_INT8_TOPS, "frac": round(achieved / PRACTICAL_INT8_TOPS, 4),

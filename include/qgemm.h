@@ -82,7 +82,10 @@ QGEMM_API int qgemm_mm_packed(const void *packed_a, const void *packed_b, float 
  * with qgemm_pack_b(range 127); every call quantizes A (op_mm.cuh:76-77, 82-87) and runs the int8 GEMM
  * with the fused dequantize (op_mm.cuh:92-99) -- bit-identical to op_mm_quantize(A, B, C, m, n, k) on the
  * B that was packed.  A: m x k (row stride a_stride_h, unit column stride), C: m x n (row stride
- * c_stride_h).  The plain form uses the library's workspace and the null stream. */
+ * c_stride_h).  The plain form uses the library's workspace and the null stream.
+ * Range: A is quantized with range 127 and O dequantized with fl(1/127^2), as op_mm_quantize does, so
+ * packed_b must come from qgemm_pack_b(..., range = 127, ...); a B packed with another range gives
+ * results that differ from op_mm_quantize (the packed buffer does not record its range). */
 QGEMM_API int op_mm_quantize_prepacked(const float *A, const void *packed_b, float *C, int m, int n, int k);
 QGEMM_API size_t op_mm_quantize_prepacked_workspace_size(int m, int n, int k);
 QGEMM_API int op_mm_quantize_prepacked_ws(const float *A, int64_t a_stride_h, const void *packed_b, float *C,

@@ -53,6 +53,12 @@ QGEMM_API int qgemm_comm_destroy(void *comm);
  * rank holds all m rows.  m % world == 0: one ncclAllGather (send buffer = C + m0*n inside the receive
  * buffer); otherwise one ncclBroadcast per owner inside a group.  Enqueued on `stream`. */
 QGEMM_API int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, void *comm, void *stream);
+/* The collectives qgemm_allgather_rows enqueues, as data (no GPU, no RCCL): returns the number of operations
+ * (0 when there is nothing to move; at most world) or -hipErrorInvalidValue.  Operation i moves count[i]
+ * floats starting at element first[i] of C: root[i] == -1 is ONE in-place all-gather (rank r sends
+ * C + first[i] + r*count[i], everyone receives C + first[i] .. + world*count[i]); root[i] >= 0 is an
+ * in-place broadcast of [first[i], first[i] + count[i]) from rank root[i]. */
+QGEMM_API int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count, int *root, int max_ops);
 
 /* One process, ndev GPUs (the harness's -g): the whole-node C4 step.  mode 0: every device's shard
  * (op_mm_quantize_shard on devices[r] with A[r], B[r], C[r], streams[r]); mode 1: the shards, then the

@@ -5,7 +5,7 @@
 #include <vector>
 #include <algorithm>
 
-#include "../csrc/attention.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/attention.hip"
 
 using namespace qgemm;
 

@@ -11,8 +11,8 @@
 #include <hip/hip_ext.h>
 
 #define QGEMM_LAB 1
-#include "../csrc/pack.hip"
-#include "../csrc/gemm_i8_kernels.h"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;

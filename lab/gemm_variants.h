@@ -4,7 +4,7 @@
 
 #include <type_traits>
 
-#include "../csrc/gemm_i8_kernels.h"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
 
 namespace qgemm {
 namespace gemm {

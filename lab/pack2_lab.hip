@@ -12,7 +12,7 @@
 #include <functional>
 #include <cstring>
 
-#include "../csrc/pack.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
 
 namespace qgemm {
 namespace {

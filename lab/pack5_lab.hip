@@ -13,7 +13,7 @@
 #include <cstring>
 
 #define QGEMM_LAB 1
-#include "../csrc/pack.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
 
 using namespace qgemm;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)

@@ -10,7 +10,7 @@
 
 #include <hip/hip_ext.h>
 
-#include "../csrc/pack.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
 
 namespace qgemm {
 namespace {

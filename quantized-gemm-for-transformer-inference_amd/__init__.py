@@ -77,6 +77,7 @@ DIST_EXPORTED_SYMBOLS = (
     "qgemm_comm_init_all",
     "qgemm_comm_destroy",
     "qgemm_allgather_rows",
+    "qgemm_allgather_plan",
     "qgemm_node_mm_quantize",
 )
 COMM_ID_BYTES = 128
@@ -199,6 +200,9 @@ def load_dist() -> ctypes.CDLL:
         D.qgemm_comm_destroy.restype = i32
         D.qgemm_allgather_rows.argtypes = [vp, i32, i32, i32, i32, vp, vp]
         D.qgemm_allgather_rows.restype = i32
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        D.qgemm_allgather_plan.argtypes = [i32, i32, i32, i64p, i64p, ctypes.POINTER(i32), i32]
+        D.qgemm_allgather_plan.restype = i32
         D.qgemm_node_mm_quantize.argtypes = [vp, vp, vp, i32, i32, i32, i32, ctypes.POINTER(i32), vp, vp, i32]
         D.qgemm_node_mm_quantize.restype = i32
         _dist = D
@@ -210,6 +214,18 @@ def shard_rows(m: int, world: int, rank: int) -> tuple:
     m0, rows = ctypes.c_int(), ctypes.c_int()
     _check("qgemm_shard_rows", load_dist().qgemm_shard_rows(m, world, rank, ctypes.byref(m0), ctypes.byref(rows)))
     return m0.value, rows.value
+
+
+def allgather_plan(m: int, n: int, world: int) -> list:
+    """The collectives qgemm_allgather_rows enqueues for an m x n C over `world` ranks, as
+    [(first, count, root)]: root -1 = one in-place all-gather of `count` floats per rank starting at
+    element `first`; root >= 0 = an in-place broadcast of [first, first + count) from that rank."""
+    cap = max(1, world)
+    first, count, root = (ctypes.c_int64 * cap)(), (ctypes.c_int64 * cap)(), (ctypes.c_int * cap)()
+    ops = load_dist().qgemm_allgather_plan(m, n, world, first, count, root, cap)
+    if ops < 0:
+        raise QGemmError("qgemm_allgather_plan", -ops)
+    return [(first[i], count[i], root[i]) for i in range(ops)]
 
 
 def op_mm_quantize_shard(A, B, C, world: int, rank: int) -> None:
@@ -426,6 +442,7 @@ def linear(X, pw: Packed, bias=None, relu: bool = False, Y=None):
     import torch
     _require_device_f32(X, "X")
     assert X.stride(1) == 1 and X.shape[1] == pw.k
+    assert pw.range == DEFAULT_RANGE, f"qgemm_linear needs a weight packed with range {DEFAULT_RANGE}"
     M, K = X.shape
     N = pw.rows
     if Y is None:
@@ -444,7 +461,10 @@ def op_mm_quantize_prepacked(A, pb: Packed, C=None):
     pack_b; A quantized on every call (op_mm.cuh:76-77, 82-87), then the int8 GEMM + dequantize."""
     import torch
     _require_device_f32(A, "A")
-    assert A.stride(1) == 1 and A.shape[1] == pb.k
+    assert A.stride(1) == 1 and A.shape[1] == pb.k, "X.w == W.h"
+    # the C entry point quantizes A with range 127 and dequantizes with 1/127^2: a B packed with another
+    # range would silently differ from op_mm_quantize
+    assert pb.range == DEFAULT_RANGE, f"op_mm_quantize_prepacked needs a B packed with range {DEFAULT_RANGE}"
     M, K = A.shape
     N = pb.rows
     if C is None:
@@ -552,4 +572,3 @@ def fill_uniform(t, seed: int, lo: float = -1.0, hi: float = 1.0):
     return t
 
 
-from . import shard  # noqa: E402,F401  (M-sharding helpers; pure Python)

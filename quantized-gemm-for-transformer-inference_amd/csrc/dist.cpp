@@ -62,24 +62,52 @@ int qgemm_comm_destroy(void *comm) {
     return nccl_rc(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
 }
 
+int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count, int *root, int max_ops) {
+    if (m < 0 || n < 0 || world < 1 || max_ops < 0 || (max_ops > 0 && (!first || !count || !root)))
+        return -(int)hipErrorInvalidValue;
+    if (world == 1 || m == 0 || n == 0) return 0;
+    if (m % world == 0) {
+        // ONE in-place all-gather: rank r's send buffer is its own rows inside the receive buffer,
+        // recv + r * count, count = (m / world) * n floats per rank
+        if (max_ops < 1) return -(int)hipErrorInvalidValue;
+        first[0] = 0;
+        count[0] = (int64_t)(m / world) * n;
+        root[0] = -1;
+        return 1;
+    }
+    // unequal shards: each owner broadcasts its rows in place (owners with no rows are skipped)
+    int ops = 0;
+    for (int r = 0; r < world; ++r) {
+        int m0 = 0, rows = 0;
+        qgemm_shard_rows(m, world, r, &m0, &rows);
+        if (rows == 0) continue;
+        if (ops >= max_ops) return -(int)hipErrorInvalidValue;
+        first[ops] = (int64_t)m0 * n;
+        count[ops] = (int64_t)rows * n;
+        root[ops] = r;
+        ++ops;
+    }
+    return ops;
+}
+
 int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, void *comm, void *stream) {
     if (!C || !comm || m < 0 || n < 0 || world < 1 || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
     ncclComm_t c = static_cast<ncclComm_t>(comm);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (world == 1 || m == 0 || n == 0) return 0;
-    if (m % world == 0) {
-        // in place: rank r's send buffer is its own rows inside the receive buffer (recv + r*count)
-        const size_t count = (size_t)(m / world) * n;
-        return nccl_rc(ncclAllGather(C + (size_t)rank * count, C, count, ncclFloat32, c, s));
-    }
-    // unequal shards: each owner broadcasts its rows in place
+    // the plan (qgemm_allgather_plan, tested on the CPU) executed on RCCL; at most world operations
+    constexpr int kMaxOps = 64;
+    int64_t first[kMaxOps], count[kMaxOps];
+    int root[kMaxOps];
+    if (world > kMaxOps) return (int)hipErrorInvalidValue;
+    const int ops = qgemm_allgather_plan(m, n, world, first, count, root, kMaxOps);
+    if (ops < 0) return -ops;
+    if (ops == 0) return 0;
+    if (ops == 1 && root[0] < 0)
+        return nccl_rc(ncclAllGather(C + (size_t)rank * (size_t)count[0], C + first[0], (size_t)count[0], ncclFloat32, c, s));
     ncclResult_t r = ncclGroupStart();
-    for (int root = 0; root < world && r == ncclSuccess; ++root) {
-        int m0 = 0, rows = 0;
-        qgemm_shard_rows(m, world, root, &m0, &rows);
-        if (rows == 0) continue;
-        float *p = C + (size_t)m0 * n;
-        r = ncclBroadcast(p, p, (size_t)rows * n, ncclFloat32, root, c, s);
+    for (int i = 0; i < ops && r == ncclSuccess; ++i) {
+        float *p = C + first[i];
+        r = ncclBroadcast(p, p, (size_t)count[i], ncclFloat32, root[i], c, s);
     }
     const ncclResult_t r2 = ncclGroupEnd();
     return nccl_rc(r != ncclSuccess ? r : r2);

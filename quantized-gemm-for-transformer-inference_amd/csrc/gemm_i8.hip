@@ -101,17 +101,17 @@ __global__ __launch_bounds__(256) void zero_tickets_kernel(unsigned *__restrict_
     if (i < n) t[i] = 0u;
 }
 
-// 256 x 256 tiles: the ping-pong schedule (gemm_i8_pp<1>, lab/pp_lab.hip at 4096^3: 62.8 vs 64.2 us for
+// 256 x 256 tiles: the ping-pong schedule (gemm_i8_pp<2>: race-free staging; mode 1 measured lab/pp_lab.hip at 4096^3: 62.8 vs 64.2 us for
 // gemm_i8_v3; 8192x4096x4096 123.9 vs 127.9; 2048x16384x4096 122.1 vs 129.3; bit-identical)
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     const GemmEvents ev = take_gemm_events();
     if ((ev.start || ev.stop) && g_event_mode == 0) {
-        hipExtLaunchKernelGGL((gemm_i8_pp<1, kEpi>), grid, dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p);
+        hipExtLaunchKernelGGL((gemm_i8_pp<2, kEpi>), grid, dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p);
         return hipGetLastError();
     }
     if (ev.start) (void)hipEventRecord(ev.start, stream);
-    gemm_i8_pp<1, kEpi><<<grid, dim3(kThreads), 0, stream>>>(p);
+    gemm_i8_pp<2, kEpi><<<grid, dim3(kThreads), 0, stream>>>(p);
     hipError_t e = hipGetLastError();
     if (ev.stop) (void)hipEventRecord(ev.stop, stream);
     return e;

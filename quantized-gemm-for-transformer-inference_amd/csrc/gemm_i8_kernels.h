@@ -684,10 +684,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
 // 2-stage LDS ring (64 KiB stages).  Staging (kDma):
 //   0: the lead waves issue stage t+1 whole in R(t) (16 LDS-DMA pieces each) and wait for it after
 //      M(t) -- two slots of flight.
-//   1: the lead waves issue A of stage t+1 in R(t) (8 pieces); lag wave wn issues B rows
-//      [64wn, 64wn+64) of stage t+2 at the end of R(t), right after its own fragment reads of stage t
-//      retired (only waves wn and wn+4 read those rows: the lead one a slot earlier), and waits for
-//      B of stage t+1 with vmcnt(8) before the slot's barrier.
+//   1: (RACY, lab only) the lead waves issue A of stage t+1 in R(t); lag wave wn issues B rows
+//      [64wn, 64wn+64) of stage t+2 at the end of R(t).  The lead's A pieces for rows 128-255 land
+//      in the buffer whose sub-step-1 A fragments the lag waves are still reading inside M(t-1) in
+//      the same slot: correct only while the DMA is slower than ~28 MFMAs.
+//   2: (product) every wave stages only rows that it and its SIMD partner, or its own half, read,
+//      each after the last reads of the slot it overwrites:
+//        lead wn, R(t):  A rows [32wn, 32wn+32) and B rows [64wn, 64wn+32) of stage t+1 (8 pieces),
+//                        waited for (vmcnt(0)) after M(t);
+//        lag wn,  R(t):  A rows [128+32wn, ..+32) of stage t+1 at the start of the slot (its own
+//                        half's last reads of that buffer were in M(t-1), a barrier ago), waited for
+//                        (vmcnt(4)) after M(t); B rows [64wn+32, 64wn+64) of stage t+2 after its own
+//                        fragment reads of stage t retired (lgkmcnt(0)), waited for (vmcnt(8)) at the
+//                        end of R(t+1).
 // Every ds_read of a stage comes a barrier after the issuing wave's covering vmcnt; every LDS-DMA
 // into a slot comes after the barrier that follows the last reads of it (lgkmcnt(0) before each
 // R-slot barrier).  Barrier counts match: lead 1 + 2nk, lag 2 + 2nk - 1.
@@ -745,6 +754,21 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
             __builtin_amdgcn_global_load_lds((const void *)(blk + (int64_t)q * 8 * kp + (int64_t)kt * BK + voff[i & 1]),
                                              (void *)(dst + q * 8 * BK), 16, 0, 0);
         }
+    };
+    auto pieces4 = [&](const int8_t *blk, int q0, int kt, int8_t *dst) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = q0 + i;  // q0 even: piece parity = i & 1
+            __builtin_amdgcn_global_load_lds((const void *)(blk + (int64_t)q * 8 * kp + (int64_t)kt * BK + voff[i & 1]),
+                                             (void *)(dst + q * 8 * BK), 16, 0, 0);
+        }
+    };
+    // mode 2: this wave's A rows (its half: lead rows 0-127, lag rows 128-255) / its B half-strip
+    auto stageA_own = [&](int kt, int buf) __attribute__((always_inline)) {
+        pieces4(Ablk, 16 * wm + 4 * wn, kt, lds + buf * kStageBytes);
+    };
+    auto stageB_half = [&](int kt, int buf) __attribute__((always_inline)) {
+        pieces4(Bblk, 8 * wn + 4 * wm, kt, lds + buf * kStageBytes + kTileBytes);
     };
     auto stageA = [&](int kt, int buf) __attribute__((always_inline)) {
         pieces8(Ablk, 8 * wn, kt, lds + buf * kStageBytes);
@@ -821,8 +845,17 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // prologue: stage 0 (+ B of stage 1 in mode 1) -> B0
-    if constexpr (kDma == 0) {
+    // prologue: stage 0 (+ B of stage 1 in mode 1, the lag's B half of stage 1 in mode 2) -> B0
+    if constexpr (kDma == 2) {
+        stageA_own(0, 0);
+        stageB_half(0, 0);
+        if (!lead && nk > 1) {
+            stageB_half(1, 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    } else if constexpr (kDma == 0) {
         if (lead) {
             stageA(0, 0);
             stageB(0, 0);
@@ -847,12 +880,32 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
     for (int t = 0; t < nk; ++t) {
         const int cur = t & 1;
         // ---- R(t)
-        if (lead && t + 1 < nk && (!(kFlags & kPPNoDma) || t == 0)) {
+        const bool dma = !(kFlags & kPPNoDma) || t == 0;
+        if constexpr (kDma == 2) {
+            if (t + 1 < nk && dma) {
+                stageA_own(t + 1, cur ^ 1);
+                if (lead) stageB_half(t + 1, cur ^ 1);
+            }
+        } else if (lead && t + 1 < nk && dma) {
             stageA(t + 1, cur ^ 1);
             if constexpr (kDma == 0) stageB(t + 1, cur ^ 1);
         }
         read_r(cur);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (kDma == 2) {
+            // lag: B half of stage t+2 over the rows just read; then B half of stage t+1 must have landed
+            // (the lead reads it in R(t+1), the next slot)
+            if (!lead) {
+                if (t + 2 < nk && !(kFlags & kPPNoDma)) {
+                    stageB_half(t + 2, cur);
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                } else if (t + 1 < nk && dma) {
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            }
+        }
         if constexpr (kDma == 1) {
             if (!lead) {
                 if (t + 2 < nk && !(kFlags & kPPNoDma)) {
@@ -870,6 +923,11 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             barrier();
         } else if (t + 1 < nk) {
+            if constexpr (kDma == 2) {
+                // lag: its A rows of stage t+1 (issued in R(t)) land before the barrier ahead of R(t+1)
+                if (t + 2 < nk && !(kFlags & kPPNoDma)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             barrier();
         }
     }

@@ -223,6 +223,9 @@ size_t outlier_scratch_bytes(int m, int n, int k) {
 hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
                         PackedView va, PackedView vb, float range, hipStream_t s) {
     if (!gemm_outlier_ok(m, n, (int)va.k_pad) || !pack_single_pass_outlier_ok(X, k, m, k, W, n, n)) return hipErrorNotSupported;
+    // xo / wo (offsets of a256 from the scratch) are read and written as float4: a scratch that is not 16-B
+    // aligned takes the materialising fallback before anything is enqueued
+    if (reinterpret_cast<uintptr_t>(scratch) % 16 != 0) return hipErrorNotSupported;
     const OutlierScratch v = scratch_view(scratch, m, k);
     const int64_t wo_ld = round_up(n, 256);
     hipError_t e = outlier_scan(X, k, m, k, t, v, s);

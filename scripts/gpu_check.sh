@@ -24,7 +24,7 @@ for s in $STEPS; do
     benchq) run benchq 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-error-stats ;;
     timing) run timing 600 quantized-gemm-for-transformer-inference_amd/build/timing_quantize -m 4096 -n 4096 -k 4096 -r 3 ;;
-    lab)    run lab 300 quantized-gemm-for-transformer-inference_amd/build/gemm_lab 4096 4096 4096 5 ;;
+    lab)    run lab 300 lab/build/gemm_lab 4096 4096 4096 5 ;;
     *) echo "unknown step $s";;
   esac
 done

@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc; mkdir -p $OUT
-LAB=quantized-gemm-for-transformer-inference_amd/build/gemm_lab
+LAB=lab/build/gemm_lab
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 for V in ${VARIANTS:-v3p_nostore v5_s3}; do
   i=0

@@ -4,7 +4,7 @@
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-B=quantized-gemm-for-transformer-inference_amd/build/pack2_lab
+B=lab/build/pack2_lab
 for s in "512 8192 4096" "512 16384 4096"; do
   tag=$(echo $s | tr ' ' x)
   timeout -s KILL 90 rocprofv3 --pmc ${PMC:-TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_MULTI_MISS_sum} -d gpurun_out/pmc_tlb_$tag -o run --output-format csv -- $B $s 3 > gpurun_out/pmc_tlb_$tag.log 2>&1

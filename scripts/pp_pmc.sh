@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pp_pmc; mkdir -p $OUT
-L=quantized-gemm-for-transformer-inference_amd/build/pp_lab
+L=lab/build/pp_lab
 timeout -k 10 120 $L 4096 4096 4096 0 clock > $OUT/clock.log 2>&1; echo "clock rc=$?"; cat $OUT/clock.log
 timeout -k 10 120 $L 4096 4096 4096 5 v3p,pp1,pp1_nostore,pp1_nodma_ns > $OUT/abl.log 2>&1; echo "abl rc=$?"; grep -v check $OUT/abl.log
 P="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"

@@ -18,7 +18,7 @@ if [ -n "${LAB:-}" ]; then
   for s in $LAB; do
     IFS=x read m n k <<< "$s"
     echo "== lab clock $m $n $k"
-    timeout -k 10 200 quantized-gemm-for-transformer-inference_amd/build/gemm_lab $m $n $k 0 clock > $OUT/labclock_$s.log 2>&1
+    timeout -k 10 200 lab/build/gemm_lab $m $n $k 0 clock > $OUT/labclock_$s.log 2>&1
     cat $OUT/labclock_$s.log
   done
 fi

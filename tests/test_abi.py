@@ -119,18 +119,16 @@ def test_dist_library_exports_every_declared_symbol(qg):
 
 
 def test_shard_rows_partition_without_gpu(qg):
-    """qgemm_shard_rows: contiguous, balanced (sizes differ by <= 1), covering, = shard.row_range."""
-    import importlib
-    shard = importlib.import_module("qgemm_amd.shard")
+    """qgemm_shard_rows: contiguous, balanced (sizes differ by <= 1), covering."""
     for m in (0, 1, 7, 255, 4096, 65536, 65537):
         for world in (1, 2, 3, 4, 8):
-            nxt = 0
+            nxt, sizes = 0, []
             for r in range(world):
                 m0, rows = qg.shard_rows(m, world, r)
                 assert m0 == nxt and rows >= 0
-                assert (m0, m0 + rows) == shard.row_range(m, world, r)
                 nxt = m0 + rows
-            assert nxt == m
+                sizes.append(rows)
+            assert nxt == m and max(sizes) - min(sizes) <= 1
     D = qg.load_dist()
     a, b = ctypes.c_int(), ctypes.c_int()
     assert D.qgemm_shard_rows(8, 2, 2, ctypes.byref(a), ctypes.byref(b)) == 1  # rank >= world
@@ -138,3 +136,51 @@ def test_shard_rows_partition_without_gpu(qg):
     # argument checks before any device work
     assert D.op_mm_quantize_shard(None, None, None, 8, 8, 8, 2, 0, None) == 1
     assert D.qgemm_allgather_rows(None, 8, 8, 2, 0, None, None) == 1
+
+
+def _simulate_plan(plan, m, n, world, qg):
+    """Execute qgemm_allgather_rows' collectives on `world` simulated ranks (numpy buffers), each starting
+    with only its own shard's rows set: returns the ranks' buffers afterwards."""
+    import numpy as np
+    full = np.arange(m * n, dtype=np.float64) + 1
+    bufs = []
+    for r in range(world):
+        b = np.zeros(m * n)
+        m0, rows = qg.shard_rows(m, world, r)
+        b[m0 * n:(m0 + rows) * n] = full[m0 * n:(m0 + rows) * n]
+        bufs.append(b)
+    for first, count, root in plan:
+        if root < 0:  # in-place all-gather: rank r's send buffer is recv + r * count
+            sent = [bufs[r][first + r * count:first + (r + 1) * count].copy() for r in range(world)]
+            for b in bufs:
+                for r in range(world):
+                    b[first + r * count:first + (r + 1) * count] = sent[r]
+        else:
+            src = bufs[root][first:first + count].copy()
+            for b in bufs:
+                b[first:first + count] = src
+    return full, bufs
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 7, 8])
+def test_allgather_plan_reassembles_every_rank(qg, world):
+    """The collectives qgemm_allgather_rows enqueues (qgemm_allgather_plan), run on simulated ranks: every
+    rank ends with all m rows, for m % world == 0 (one in-place all-gather) and != 0 (one broadcast per
+    owner; empty owners skipped), including m < world."""
+    import numpy as np
+    for m in (0, 1, 3, 8, 24, 65, 96, 1001):
+        n = 5
+        plan = qg.allgather_plan(m, n, world)
+        if world == 1 or m == 0:
+            assert plan == []
+            continue
+        if m % world == 0:
+            assert plan == [(0, m // world * n, -1)]
+        else:
+            assert all(root >= 0 for _, _, root in plan) and len(plan) == min(m, world)
+        full, bufs = _simulate_plan(plan, m, n, world, qg)
+        for r, b in enumerate(bufs):
+            assert np.array_equal(b, full), f"m={m} world={world} rank {r}"
+    D = qg.load_dist()
+    assert D.qgemm_allgather_plan(-1, 4, 2, None, None, None, 0) < 0
+    assert D.qgemm_allgather_plan(8, 4, 2, None, None, None, 0) < 0  # one op needed, no room

@@ -69,3 +69,34 @@ def test_timing_quantize_prints_the_reference_lines():
     assert len(avg) == 2 and all(a > 0 for a in avg)
     js = json.loads(out[i + 2])
     assert js["m"] == 2048 and js["quantized_gemms_per_s"] > 0
+
+
+def test_one_rccl_with_torch_process_group(qg, device):
+    """bench.py --gpus N runs torch's RCCL process group (barriers, MAX all-reduce) beside libqgemm_dist.so's
+    own communicator (the C4 all-gather).  Both RCCL builds carry the soname librccl.so.1, so the dynamic
+    loader must satisfy libqgemm_dist.so's NEEDED entry with the copy torch already mapped: exactly one
+    librccl in the process, the one torch loaded."""
+    import socket
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(device))
+    try:
+        t = torch.ones(4, device=device)
+        dist.all_reduce(t)
+        comm = qg.Comm(1, 0, qg.Comm.unique_id())
+        try:
+            C = torch.arange(16 * 8, dtype=torch.float32, device=device).reshape(16, 8)
+            comm.allgather_rows(C)
+            torch.cuda.synchronize()
+        finally:
+            comm.close()
+        maps = open("/proc/self/maps").read().splitlines()
+        rccl = sorted({ln.split()[-1] for ln in maps if "librccl" in ln.split()[-1]})
+        print("mapped RCCL:", rccl)
+        assert len(rccl) == 1, f"{len(rccl)} RCCL libraries mapped: {rccl}"
+        assert "torch" in rccl[0], rccl
+    finally:
+        dist.destroy_process_group()

@@ -138,3 +138,46 @@ def test_outlier_edges(qg, oracle, device, M, N, K, t):
         assert cnt == 0
         assert_bits_equal(want, oracle.quantized_mm(X, W), "oracle: no outliers = plain path")
     assert_bits_equal(C.cpu().numpy(), want, f"outlier edge {M}x{N}x{K} t={t}")
+
+
+def _bench_outliers(oracle, M, N, K, ncols, seed):
+    """bench.py's c2_outlier placement: ncols feature columns spread over K ((K // ncols) * c + 7c + 3),
+    |x| in 7..60 with random signs in every 50th row."""
+    X, W = oracle.inputs(M, N, K, seed)
+    rng = np.random.default_rng(seed)
+    cols = [(K // ncols) * c + 7 * c + 3 for c in range(ncols)]
+    for c in cols:
+        n = X[::50, c].size
+        X[::50, c] = (rng.uniform(7, 60, n) * rng.choice([-1.0, 1.0], n)).astype(np.float32)
+    return X, W, cols
+
+
+@pytest.mark.parametrize("ncols", [8, 32])
+def test_outlier_fast_path_at_the_benched_shape(qg, oracle, device, ncols):
+    """The advertised c2_outlier shape, 4096^3 with K = 4096, every output bit: 8 outlier columns take the
+    LDS-staged chain in the GEMM epilogue (<= kOutlierStaged), 32 the global-memory chain."""
+    M = N = K = 4096
+    X, W, cols = _bench_outliers(oracle, M, N, K, ncols, 17 + ncols)
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    assert cnt == wcnt == ncols
+    assert_bits_equal(C.cpu().numpy(), want, f"outlier 4096^3, {ncols} columns")
+
+
+def test_outlier_unaligned_workspace_takes_the_fallback(qg, oracle, device):
+    """A caller workspace that is only 4-B aligned: the fast path's float4 xo / wo accesses cannot run on
+    it, so the call takes the materialising fallback (nothing enqueued first) and stays bit-exact."""
+    M, N, K = 2560, 4096, 256
+    X, W = _with_outliers(oracle, M, N, K, [1, 100, 255], 14)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    L = qg.load()
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    need = L.qgemm_mm_outlier_workspace_size(M, N, K)
+    buf = torch.empty(need + 256, dtype=torch.uint8, device=device)
+    O = torch.full((M, N), float("nan"), device=device)
+    s = qg._stream(device)
+    assert L.qgemm_mm_outlier(Xd.data_ptr(), Wd.data_ptr(), O.data_ptr(), M, N, K, 6.0, buf.data_ptr() + 4, need,
+                              s) == 0
+    torch.cuda.synchronize()
+    assert wcnt == 3
+    assert_bits_equal(O.cpu().numpy(), want, "outlier, 4-B aligned workspace")

@@ -464,3 +464,22 @@ def test_lds_dma_rings_repeat_race_screen(qg, oracle, device):
     torch.cuda.synchronize()
     for i, C in enumerate(outs):
         assert_bits_equal(C.cpu().numpy(), want, f"fp32 {M}x{N}x{K} repeat {i}")
+
+
+@pytest.mark.parametrize("K", [128, 256, 384, 640])
+def test_pingpong_ring_l2_hot_repeat(qg, oracle, device, K):
+    """Race screen of the 256-tile ping-pong GEMM's LDS ring with the DMA source hot in L2: 256 tiles
+    (no split-K), one to five k-steps, so every panel is tiny and re-read by the XCD's other tiles and
+    the LDS-DMA lands as fast as it can; 20 back-to-back calls, every output bit.  (Staging mode 1 let
+    a lead wave's DMA overwrite A rows a lag wave was still reading: wrong whenever the DMA beats
+    ~28 MFMAs -- ADVICE r2.)"""
+    M = N = 4096
+    X, W = oracle.inputs(M, N, K, 131)
+    want = oracle.quantized_mm(X, W)
+    pa, pb = qg.pack_a(_dev(X, device)), qg.pack_b(_dev(W, device))
+    outs = [torch.empty((M, N), device=device) for _ in range(20)]
+    for O in outs:
+        qg.mm_packed(pa, pb, O)
+    torch.cuda.synchronize()
+    for i, O in enumerate(outs):
+        assert_bits_equal(O.cpu().numpy(), want, f"4096x4096x{K} repeat {i}")

@@ -22,16 +22,3 @@ def test_packed_geometry(qg):
     assert (p.rows_pad, p.k_pad) == (512, 256)
     assert p.scale.numel() == 512 and p.scale.dtype == torch.float32
     assert tuple(p.q.shape) == (512, 256) and p.q.dtype == torch.int8
-
-
-def test_shard_rows_cover_exactly(qg):
-    from importlib import import_module  # noqa: F401
-    shard = qg.shard
-    for M in (1, 7, 8, 4096, 65536, 65537):
-        for world in (1, 2, 3, 4, 8):
-            ranges = [shard.row_range(M, world, r) for r in range(world)]
-            assert ranges[0][0] == 0 and ranges[-1][1] == M
-            for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
-                assert a1 == b0 and a0 <= a1
-            sizes = [b - a for a, b in ranges]
-            assert max(sizes) - min(sizes) <= 1
