@@ -153,6 +153,28 @@ def outlier_columns(K):
     return [(K // OUTLIER_COLS) * c + 7 * c + 3 for c in range(OUTLIER_COLS)], 50
 
 
+def host_cpu_share():
+    """The host cores this process may use, measured: the affinity mask (os.sched_getaffinity), the cgroup
+    CPU quota (cpu.max: quota / period), and OMP_NUM_THREADS if the environment pins it; the thread count
+    is the smallest of them (the box's CPU share), reported with where it came from."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    cands = [("affinity", aff)]
+    if quota:
+        cands.append(("cgroup cpu.max", max(1, int(quota))))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        cands.append(("OMP_NUM_THREADS", int(env)))
+    src, n = min(cands, key=lambda c: c[1])
+    return {"threads": n, "source": src, "affinity": aff, "quota": quota}
+
+
 def cpu_baseline(M, N, K, target_s, outlier=False):
     """Time the oracle's quantized chain (and the unquantized fp32 GEMM) on the host cores.
 
@@ -160,7 +182,9 @@ def cpu_baseline(M, N, K, target_s, outlier=False):
     M=N=K=4096 chain in well under a second on 16 cores); the fp32 path runs once on the full problem."""
     from oracle import oracle as O
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cpu = host_cpu_share()
+    threads = cpu["threads"]
+    O.set_threads(threads)
     X, W = O.uniform((M, K), 0), O.uniform((K, N), 1)
     if outlier:
         cols, every = outlier_columns(K)
@@ -184,6 +208,9 @@ def cpu_baseline(M, N, K, target_s, outlier=False):
         "value": reps / tq,
         "unit": "GEMMs/s",
         "cores": threads,
+        "cores_source": cpu["source"],
+        "affinity_cpus": cpu["affinity"],
+        "cgroup_cpu_quota": cpu["quota"],
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
         "kind": "port",
@@ -575,6 +602,8 @@ def bench_encoder(args, qg, L, dev, world, rank, distributed):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
         O.build()
+        cpu = host_cpu_share()
+        O.set_threads(cpu["threads"])
         Xh = O.uniform((seq, d), 2 * 1000)
         O.encoder_forward(Xh, d, H, dff, 1, 1000)  # warm
         reps, tc = 0, 0.0
@@ -585,7 +614,7 @@ def bench_encoder(args, qg, L, dev, world, rank, distributed):
             reps += 1
         result["cpu_baseline"] = {
             "value": reps / tc, "unit": "forwards/s",
-            "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), "kind": "port",
+            "cores": cpu["threads"], "cores_source": cpu["source"], "affinity_cpus": cpu["affinity"], "kind": "port",
             "sample": f"oracle/ C restatement of the encoder (transformer.cu:14-77 with quantized linears), "
                       f"full config-5 forward x{reps} = {tc:.1f} s",
         }

@@ -1,0 +1,153 @@
+// w4_lab.hip -- LAB harness: the 4-wave 128x128-wave-tile GEMM (gemm_w4.h) against the product ping-pong
+// kernel, bit-checked and timed in interleaved rounds in one process; `clock` mode: in-kernel loop clocks.
+//   build/w4_lab m n k rounds [names|clock]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+#include <string>
+#include <cstring>
+
+#define QGEMM_LAB 1
+#include "gemm_w4.h"
+
+using namespace qgemm;
+using namespace qgemm::gemm;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+__global__ void fill_i8(int8_t *p, int64_t n, uint64_t seed) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = (int8_t)((int)(mix64(seed + i) >> 56) - 128);
+}
+__global__ void fill_f(float *p, int64_t n, uint64_t seed) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = 0.5f + (float)(mix64(seed + i) >> 40) * (1.0f / 16777216.0f);
+}
+
+typedef void (*KernelFn)(GemmArgs);
+struct Variant { const char *name; KernelFn fn; int threads; bool flayout = false; };
+
+int main(int argc, char **argv) {
+    int m = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 4096;
+    int rounds = argc > 4 ? atoi(argv[4]) : 5, reps = 20;
+    const char *only = argc > 5 ? argv[5] : nullptr;
+    int64_t mp = round_up(m, 256), np_ = round_up(n, 256), kp = round_up(k, 128);
+    int8_t *A, *B; float *Cx, *Cw, *C, *Cref;
+    CK(hipMalloc(&A, mp * kp)); CK(hipMalloc(&B, np_ * kp));
+    CK(hipMalloc(&Cx, mp * 4)); CK(hipMalloc(&Cw, np_ * 4));
+    CK(hipMalloc(&C, (size_t)m * n * 4)); CK(hipMalloc(&Cref, (size_t)m * n * 4));
+    fill_i8<<<4096, 256>>>(A, mp * kp, 1); fill_i8<<<4096, 256>>>(B, np_ * kp, 2);
+    fill_f<<<64, 256>>>(Cx, mp, 3); fill_f<<<64, 256>>>(Cw, np_, 4);
+    CK(hipDeviceSynchronize());
+    GemmArgs p{A, B, Cx, Cw, C, n, 1, m, n, kp, (int)(mp / BM), (int)(np_ / BN), 1.0f / (127.0f * 127.0f)};
+    int8_t *AF, *BF;
+    CK(hipMalloc(&AF, mp * kp)); CK(hipMalloc(&BF, np_ * kp));
+    relayout_f_kernel<<<(unsigned)((mp / 16) * (kp / 64) / 4), 256>>>(A, AF, mp, kp);
+    relayout_f_kernel<<<(unsigned)((np_ / 16) * (kp / 64) / 4), 256>>>(B, BF, np_, kp);
+    CK(hipDeviceSynchronize());
+    GemmArgs pf = p; pf.A = AF; pf.B = BF;
+    std::vector<Variant> vs = {
+        {"pp2", gemm_i8_pp<2>, 512},
+        {"pp2_nostore", gemm_i8_pp<2, kEpiNone, kPPNoStore>, 512},
+        {"w4", gemm_i8_w4<kW4PadT>, 256},
+        {"w4_t256", gemm_i8_w4<0>, 256},
+        {"w4_nostore", gemm_i8_w4<kW4PadT | kW4NoStore>, 256},
+        {"w4_nodma_ns", gemm_i8_w4<kW4PadT | kW4NoStore | kW4NoDma>, 256},
+        {"w4_noread_ns", gemm_i8_w4<kW4PadT | kW4NoStore | kW4NoRead>, 256},
+        {"w4_bare_ns", gemm_i8_w4<kW4PadT | kW4NoStore | kW4NoRead | kW4NoDma>, 256},
+        {"w4s", gemm_i8_w4s<0>, 256},
+        {"w4s_nostore", gemm_i8_w4s<kW4NoStore>, 256},
+        {"w4s_nodma_ns", gemm_i8_w4s<kW4NoStore | kW4NoDma>, 256},
+        {"f4", gemm_i8_f4<0>, 256, true},
+        {"f4_nostore", gemm_i8_f4<kW4NoStore>, 256, true},
+        {"f4rm", gemm_i8_f4<kW4RowMajor>, 256, false},
+        {"f4_noload_ns", gemm_i8_f4<kW4NoStore | kW4NoRead>, 256, true},
+    };
+    dim3 grid(p.tiles_m * p.tiles_n);
+    if (only && std::string(only) == "clock") {
+        struct SV { const char *name; KernelFn fn; int threads; unsigned long long *sym; };
+        unsigned long long *pp_sym, *w4_sym;
+        CK(hipGetSymbolAddress((void **)&pp_sym, HIP_SYMBOL(g_pp_stamp)));
+        CK(hipGetSymbolAddress((void **)&w4_sym, HIP_SYMBOL(g_w4_stamp)));
+        std::vector<SV> sv = {
+            {"pp2", gemm_i8_pp<2, kEpiNone, kPPStamp>, 512, pp_sym},
+            {"w4", gemm_i8_w4<kW4PadT | kW4Stamp>, 256, w4_sym},
+            {"w4_nostore", gemm_i8_w4<kW4PadT | kW4Stamp | kW4NoStore>, 256, w4_sym},
+            {"w4_bare_ns", gemm_i8_w4<kW4PadT | kW4Stamp | kW4NoStore | kW4NoRead | kW4NoDma>, 256, w4_sym},
+            {"w4s", gemm_i8_w4s<kW4Stamp>, 256, w4_sym},
+            {"w4s_nostore", gemm_i8_w4s<kW4Stamp | kW4NoStore>, 256, w4_sym},
+            {"f4", gemm_i8_f4<kW4Stamp>, 256, w4_sym},
+            {"f4_nostore", gemm_i8_f4<kW4Stamp | kW4NoStore>, 256, w4_sym},
+        };
+        const int nb = p.tiles_m * p.tiles_n;
+        for (auto &v : sv) {
+            hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
+            int launches = 0; float ms = 0;
+            CK(hipEventRecord(a));
+            while (ms < 2000) {
+                for (int i = 0; i < 200; ++i) v.fn<<<grid, v.threads>>>(strncmp(v.name, "f4", 2) == 0 ? pf : p);
+                launches += 200;
+                CK(hipEventRecord(z)); CK(hipEventSynchronize(z)); CK(hipEventElapsedTime(&ms, a, z));
+            }
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned long long> st((size_t)4096 * 6);
+            CK(hipMemcpy(st.data(), v.sym, st.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> lc, lu, ec, eu;
+            for (int i = 0; i < nb; ++i) {
+                const unsigned long long *q = &st[(size_t)i * 6];
+                lc.push_back((double)(q[2] - q[0]) / (double)(q[3] - q[1]) * 0.1);
+                lu.push_back((double)(q[3] - q[1]) * 0.01);
+                ec.push_back((double)(q[4] - q[2]) / std::max(1.0, (double)(q[5] - q[3])) * 0.1);
+                eu.push_back((double)(q[5] - q[3]) * 0.01);
+            }
+            auto med = [](std::vector<double> x) { std::sort(x.begin(), x.end()); return x[x.size() / 2]; };
+            printf("%-14s avg launch %7.2f us  loop: clock %.3f GHz, %6.2f us/block  epilogue: clock %.3f GHz, %6.2f us/block\n",
+                   v.name, ms * 1000 / launches, med(lc), med(lu), med(ec), med(eu));
+        }
+        return 0;
+    }
+    if (only) {
+        std::vector<Variant> keep;
+        const std::string list = std::string(",") + only + ",";
+        for (auto &v : vs)
+            if (list.find(std::string(",") + v.name + ",") != std::string::npos) keep.push_back(v);
+        vs = keep;
+    }
+    GemmArgs pr = p; pr.C = Cref;
+    gemm_i8_pp<2><<<grid, 512>>>(pr);
+    CK(hipDeviceSynchronize());
+    std::vector<float> href((size_t)m * n), hgot((size_t)m * n);
+    CK(hipMemcpy(href.data(), Cref, href.size() * 4, hipMemcpyDeviceToHost));
+    for (auto &v : vs) {
+        if (strstr(v.name, "_ns") || strstr(v.name, "nostore")) continue;
+        for (int rep = 0; rep < 3; ++rep) {
+            CK(hipMemset(C, 0xff, (size_t)m * n * 4));
+            v.fn<<<grid, v.threads>>>(v.flayout ? pf : p);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t i = 0; i < href.size(); ++i) bad += memcmp(&href[i], &hgot[i], 4) != 0;
+            printf("check %-12s rep %d mismatches %zu\n", v.name, rep, bad);
+        }
+    }
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> t(vs.size());
+    for (int r = 0; r < rounds; ++r)
+        for (size_t vi = 0; vi < vs.size(); ++vi) {
+            const GemmArgs &pv = vs[vi].flayout ? pf : p;
+            for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, vs[vi].threads>>>(pv);
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, vs[vi].threads>>>(pv);
+            CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            t[vi].push_back(ms * 1000 / reps);
+        }
+    double ops = 2.0 * m * n * (double)k;
+    for (size_t vi = 0; vi < vs.size(); ++vi) {
+        auto v = t[vi]; std::sort(v.begin(), v.end());
+        printf("%-14s median %8.2f us  min %8.2f us  %7.1f TOPS  %5.1f%% of 5033\n", vs[vi].name, v[v.size() / 2], v[0],
+               ops / (v[v.size() / 2] * 1e-6) / 1e12, 100 * ops / (v[v.size() / 2] * 1e-6) / 1e12 / 5033.2);
+    }
+    return 0;
+}

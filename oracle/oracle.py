@@ -72,6 +72,7 @@ def lib():
             L.oracle_encoder_weight_seed.restype = _c_u64
             L.oracle_encoder_weight_seed.argtypes = [_c_u64, _c_int, _c_int, _c_int]
             L.oracle_encoder_forward.argtypes = [_f32p, _f32p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_u64]
+            L.oracle_set_threads.argtypes = [_c_int]
             L.oracle_mm_outlier.restype = _c_int
             L.oracle_mm_outlier.argtypes = [_f32p, _f32p, _f32p, _c_int, _c_int, _c_int, _c_f]
             _lib = L
@@ -83,6 +84,11 @@ def _c(a, dtype):
 
 
 # ----------------------------------------------------------------------------- inputs
+def set_threads(n: int) -> None:
+    """OpenMP thread count of the restatement's parallel loops (bench.py cpu_baseline)."""
+    lib().oracle_set_threads(int(n))
+
+
 def uniform(shape, seed: int, lo: float = -1.0, hi: float = 1.0) -> np.ndarray:
     """Seeded U[lo,hi) fp32 matrix, bit-identical to the HIP fill kernel (qgemm_fill_uniform)."""
     n = int(np.prod(shape))

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
+#include <omp.h>
 
 #define ORACLE_TILE 32 /* TILE_WIDTH, op_mm.cuh:6 -- sets the zero-padding of the fp32 k loop */
 
@@ -525,4 +526,10 @@ int oracle_mm_outlier(const float *X, const float *W, float *O, int M, int N, in
     free(Xm);
     free(Wm);
     return cnt;
+}
+
+/* The thread count of the OpenMP regions above (bench.py's cpu_baseline sets it from the measured host CPU
+ * share, so `cores` is what ran, not an environment default). */
+void oracle_set_threads(int n) {
+    if (n > 0) omp_set_num_threads(n);
 }

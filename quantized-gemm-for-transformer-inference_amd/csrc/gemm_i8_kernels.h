@@ -25,6 +25,12 @@ constexpr int kThreads = 512;
 constexpr int kTileBytes = BM * BK;          // 32 KiB per operand per stage
 constexpr int kStageBytes = 2 * kTileBytes;  // A + B
 constexpr int kLdsBytes = 2 * kStageBytes;   // 2-deep ring = 128 KiB
+// epilogue16's fp32 image of a 128-row half: rows padded to 260 floats, so the ds_write_b32 of the
+// accumulators (lanes 16 apart = rows 4 apart) fall on banks 16 apart instead of the same bank (r02 PMC:
+// 6.7 % bank-conflict cycles in gemm_i8_pp); the scales and the rest of the epilogue's LDS follow it
+constexpr int kTStride = 260;
+constexpr int kTImgBytes = 128 * kTStride * 4;
+constexpr int kEpiBase = kTImgBytes > kLdsBytes ? kTImgBytes : kLdsBytes;
 
 static_assert(BM == kRowPad && BN == kRowPad && BK == kKPad, "packed layout must match the macro-tile");
 
@@ -344,7 +350,7 @@ __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const f
             for (int g = 0; g < 8; ++g) {
                 const int i = ib + 8 * g;
                 if (i >= p.m) break;
-                const float4 o = *reinterpret_cast<const float4 *>(T + (i - i0) * BN + c4);
+                const float4 o = *reinterpret_cast<const float4 *>(T + (i - i0) * kTStride + c4);
                 const float vv[4] = {__fadd_rn(o.x, c[g][0]), __fadd_rn(o.y, c[g][1]), __fadd_rn(o.z, c[g][2]),
                                      __fadd_rn(o.w, c[g][3])};
                 if (full) {
@@ -398,7 +404,7 @@ __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const f
         for (int g = 0; g < 8; ++g) {
             const int i = ib + 8 * g;
             if (i >= p.m) break;
-            const float4 o = *reinterpret_cast<const float4 *>(T + (i - i0) * BN + c4);
+            const float4 o = *reinterpret_cast<const float4 *>(T + (i - i0) * kTStride + c4);
             const float vv[4] = {__fadd_rn(o.x, c[g][0]), __fadd_rn(o.y, c[g][1]), __fadd_rn(o.z, c[g][2]),
                                  __fadd_rn(o.w, c[g][3])};
             if (full) {
@@ -428,13 +434,13 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
         if (x == 0x7fffffff && p.m < 0) static_cast<int *>(p.C)[tid] = x;
         return;
     }
-    float *sCx = reinterpret_cast<float *>(lds + kLdsBytes);
+    float *sCx = reinterpret_cast<float *>(lds + kEpiBase);
     float *sCw = sCx + BM;
-    float *sB = sCw + BN;  // bias (kEpi >= 1): needs kLdsBytes + 3 KiB
+    float *sB = sCw + BN;  // bias (kEpi >= 1): needs kEpiBase + 3 KiB
     float *C = static_cast<float *>(p.C);
     // kEpiOutlier, <= kOutlierStaged outlier columns: this tile's xo rows and wo columns are loaded here,
     // ahead of the barrier (their latency hides under the ring drain), and parked in LDS behind Cx / Cw
-    float *sX = reinterpret_cast<float *>(lds + kLdsBytes + 2048), *sW = sX + 256 * kOutlierStaged;
+    float *sX = reinterpret_cast<float *>(lds + kEpiBase + 2048), *sW = sX + 256 * kOutlierStaged;
     bool staged = false;
     float xs4[4] = {0.f, 0.f, 0.f, 0.f};
     float4 ws4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -483,7 +489,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
                 }
         }
     } else {
-        float *T = reinterpret_cast<float *>(lds);  // [128][256] fp32
+        float *T = reinterpret_cast<float *>(lds);  // [128][kTStride] fp32
         const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
                           gj0 + BN <= p.n;
 #pragma unroll
@@ -499,7 +505,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int il = mi * 16 + 4 * kq + r;
-                            T[il * BN + jl] = epi_extra<kEpi>(
+                            T[il * kTStride + jl] = epi_extra<kEpi>(
                                 dequantize(acc[mi][ni][r], outer_product(sCx[half * 128 + il], cw), p.inv_r2), sB, jl);
                         }
                 }
@@ -517,7 +523,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
             for (int rr = tid >> 6; rr < 128; rr += kThreads / 64) {
                 const int i = gi0 + half * 128 + rr;
                 if (i >= p.m) break;
-                const float4 v = *reinterpret_cast<const float4 *>(T + rr * BN + c4);
+                const float4 v = *reinterpret_cast<const float4 *>(T + rr * kTStride + c4);
                 const int j = gj0 + c4;
                 if (full) {
                     if constexpr (kNt) {
@@ -543,18 +549,18 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
 // 8 x 4 tiles; per 64-deep sub-step 8 A + 4 B fragment reads (lane l: row l&15, 16 bytes of k-chunk
 // 4s + (l>>4)) and 32 MFMAs.  C/D map: col = lane&15, row = 4(lane>>4) + reg.
 // In-launch split-K combine (cdna_hip_programming.md s5 "In-launch split-K reduction", the counter
-// form of s6 Guideline 16): every slice stores its accumulators as a slab with plain 16-B stores,
-// drains, and after the block barrier lane 0 publishes with ONE agent-scope release and draws a
-// ticket; the slice that draws S-1 is the reducer: ONE agent-scope acquire, then plain slab loads.
-// Correct for any placement of a tile's slices over XCDs/CUs.  The "last arriver" word goes through
-// the one LDS array (a second __shared__ object can de-pipeline the main loop).  Returns true in the
-// reducer, which then holds the complete sums in acc.
+// form of s6 Guideline 16), WRITE-THROUGH form: there is deliberately NO release fence and NO acquire
+// fence (do not add them back: a buffer_wbl2 also writes back every dirty line of the XCD's L2 --
+// other blocks' output tiles included -- and cost 14 us at 2048^3 split 2).  Instead
+// every slab byte is stored with sc1 (write-through) 16-B buffer stores, every storing wave drains
+// them (s_waitcnt vmcnt(0)) before the block barrier, lane 0 then draws the arrival ticket with a
+// relaxed agent-scope atomic add, and the slice that draws S-1 is the reducer, which reads the other
+// slabs with sc1 buffer loads (EVERY load of them).  Correct for any placement of a tile's slices over
+// XCDs/CUs (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores drained before the counter,
+// sc1 loads after it).  The "last arriver" word goes through the one LDS array (a second __shared__
+// object can de-pipeline the main loop).  Returns true in the reducer, which then holds the complete
+// sums in acc.
 // MI x NI accumulator tiles per wave, kWaves waves: a slab is kWaves*MI*NI*64 v4i (= the tile's int32s).
-// Publish form (cdna_hip_programming.md s5 'In-launch split-K reduction', the write-through variant):
-// slab stores are sc1 (write-through), drained by every wave before the block barrier, then lane 0
-// draws the ticket with a relaxed agent-scope add -- no release fence (a buffer_wbl2 would also write
-// back every dirty line of the XCD's L2, including other blocks' output tiles); the reducer reads
-// the other slabs with sc1 loads (every load of them), so no acquire either.
 template <int MI, int NI, int kWaves, bool kSlab = true>
 __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last, v4i (&acc)[MI][NI], int tile,
                                                int slice, int S, int wave, int lane, int tid) {
@@ -596,7 +602,7 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last
 template <int kMode, bool kDequant, int kFlags = 0, int kEpi = kEpiNone>
 __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
     // + scales (and bias) for the epilogue
-    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes + (has_bias(kEpi) ? 3072 : 2048)];
+    __shared__ __attribute__((aligned(16))) int8_t lds[kEpiBase + (has_bias(kEpi) ? 3072 : 2048)];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -662,7 +668,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
     }
 
     if (S > 1 &&
-        !splitk_combine<8, 4, 8, !(kFlags & kNoSlab)>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice,
+        !splitk_combine<8, 4, 8, !(kFlags & kNoSlab)>(p, reinterpret_cast<unsigned *>(lds + kEpiBase), acc, tile, slice,
                                                      S, wave, lane, tid))
         return;
     epilogue16<kMode, kEpi>(p, lds, acc, tm, tn, wm, wn, lane, tid);
@@ -709,7 +715,7 @@ __device__ unsigned long long g_pp_stamp[4096 * 6];
 // LDS bytes of the ping-pong body (staging ring + scales/bias/flag)
 template <int kEpi>
 constexpr int pp_lds_bytes() {
-    return kLdsBytes + (has_bias(kEpi) ? 3072 : 2048) + (kEpi == kEpiOutlier ? kOutlierStageBytes : 0);
+    return kEpiBase + (has_bias(kEpi) ? 3072 : 2048) + (kEpi == kEpiOutlier ? kOutlierStageBytes : 0);
 }
 
 // One 256 x 256 tile (k-slice `slice` of S) of the ping-pong GEMM on a 512-thread block; `lds` holds
@@ -933,7 +939,7 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
     }
 
     stamp(1);
-    if (S > 1 && !splitk_combine<8, 4, 8>(p, reinterpret_cast<unsigned *>(lds + kLdsBytes), acc, tile, slice, S, wave,
+    if (S > 1 && !splitk_combine<8, 4, 8>(p, reinterpret_cast<unsigned *>(lds + kEpiBase), acc, tile, slice, S, wave,
                                           lane, tid))
         return;
     epilogue16<(kFlags & kPPNoStore) ? kStoreNone : kStoreLds, kEpi, (kFlags & kPPNtStore) != 0>(p, lds, acc, tm, tn, wm,

@@ -141,11 +141,14 @@ def test_outlier_edges(qg, oracle, device, M, N, K, t):
 
 
 def _bench_outliers(oracle, M, N, K, ncols, seed):
-    """bench.py's c2_outlier placement: ncols feature columns spread over K ((K // ncols) * c + 7c + 3),
-    |x| in 7..60 with random signs in every 50th row."""
+    """bench.py's c2_outlier placement: ncols feature columns spread over K ((K // ncols) * c + 7c + 3 for
+    its 8 columns; the 7c offset wraps within half a stride for more), |x| in 7..60 with random signs in
+    every 50th row."""
     X, W = oracle.inputs(M, N, K, seed)
     rng = np.random.default_rng(seed)
-    cols = [(K // ncols) * c + 7 * c + 3 for c in range(ncols)]
+    stride = K // ncols
+    cols = [stride * c + (7 * c) % (stride // 2) + 3 for c in range(ncols)]
+    assert len(set(cols)) == ncols and max(cols) < K
     for c in cols:
         n = X[::50, c].size
         X[::50, c] = (rng.uniform(7, 60, n) * rng.choice([-1.0, 1.0], n)).astype(np.float32)
