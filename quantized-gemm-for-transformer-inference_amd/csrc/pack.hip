@@ -52,6 +52,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
 }
 
+// kWT (lab fused pack+GEMM launch only): the packed bytes and scales are handed to GEMM blocks of the SAME
+// launch on other XCDs, so they are stored write-through (sc1; MI355X_MICROARCH.md inter-workgroup
+// visibility) instead of staying dirty in this XCD's L2
+template <bool kWT>
+__device__ __forceinline__ void st_u32(uint32_t *p, uint32_t v) {
+    if constexpr (kWT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <bool kWT>
+__device__ __forceinline__ void st_f32(float *p, float v) {
+    if constexpr (kWT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 // The GEMM's split-K tickets live in the caller's workspace, whose contents are arbitrary: the pack
 // launch that precedes the GEMM in the same stream zeroes them (block 0), which saves the GEMM a
 // zeroing launch of its own.
@@ -80,7 +94,7 @@ __device__ __forceinline__ bool om_bit(const OutlierMask &om, int k) { return (o
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
 // R > 0: each lane keeps R float4 chunks in registers (len <= 256*R), one HBM read.
 // R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
-template <int R, bool kMask = false>
+template <int R, bool kMask = false, bool kWT = false>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
@@ -92,8 +106,8 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
     const int64_t nq = k_pad >> 2;  // uint32 words per packed row
     if (row >= rows) {              // padding row
-        for (int64_t c = lane; c < nq; c += kWave) qrow[c] = 0u;
-        if (lane == 0) scale[row] = 0.0f;
+        for (int64_t c = lane; c < nq; c += kWave) st_u32<kWT>(qrow + c, 0u);
+        if (lane == 0) st_f32<kWT>(scale + row, 0.0f);
         return;
     }
     const float *srow = src + row * sh;
@@ -187,12 +201,13 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         for (int j = 0; j < R; ++j) {
             const int c = lane + j * kWave;
             if (c < nfull)
-                qrow[c] = pack4(quant_i8(v[j].x, s), quant_i8(v[j].y, s), quant_i8(v[j].z, s), quant_i8(v[j].w, s));
+                st_u32<kWT>(qrow + c, pack4(quant_i8(v[j].x, s), quant_i8(v[j].y, s), quant_i8(v[j].z, s),
+                                            quant_i8(v[j].w, s)));
         }
     } else {
         for (int c = lane; c < nfull; c += kWave) {
             float4 x = s4[c];
-            qrow[c] = pack4(quant_i8(x.x, s), quant_i8(x.y, s), quant_i8(x.z, s), quant_i8(x.w, s));
+            st_u32<kWT>(qrow + c, pack4(quant_i8(x.x, s), quant_i8(x.y, s), quant_i8(x.z, s), quant_i8(x.w, s)));
         }
     }
     // partial tail word, then zero padding words
@@ -200,10 +215,10 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     if ((len & 3) && lane == 0) {
         int b[4] = {0, 0, 0, 0};
         for (int e = 0; e < (len & 3); ++e) b[e] = quant_i8(srow[tail0 + e], s);
-        qrow[nfull] = pack4(b[0], b[1], b[2], b[3]);
+        st_u32<kWT>(qrow + nfull, pack4(b[0], b[1], b[2], b[3]));
     }
-    for (int64_t c = first_zero + lane; c < nq; c += kWave) qrow[c] = 0u;
-    if (lane == 0) scale[row] = cx;
+    for (int64_t c = first_zero + lane; c < nq; c += kWave) st_u32<kWT>(qrow + c, 0u);
+    if (lane == 0) st_f32<kWT>(scale + row, cx);
 }
 
 // pack_rows, long rows (4096 < len <= 16384): ONE 256-thread block per row, up to 16 float4 per
@@ -774,7 +789,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
 // n = 8192 at K >= 2048, worse for wider W (n = 12288, 16384) and short K, where the 16-column pass stays.
 constexpr int kWs8Cols = 8;
 
-template <bool kMask = false>
+template <bool kMask = false, bool kWT = false>
 __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                    float range, float *__restrict__ scale, int8_t *__restrict__ q,
                                                    int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */,
@@ -861,7 +876,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
         for (int ww = 1; ww < 8; ++ww) pm = fmaxf(pm, red[ww * 8 + t]);  // -inf or >= +0: exact
         const float cw = absmax_finish(seed_masked ? 0.0f : w_seed, pm);  // seed = W[0, j] (W'[0, j])
         s_sh[t] = inv_divide(range, cw);
-        scale[n0 + t] = cw;
+        st_f32<kWT>(scale + n0 + t, cw);
     }
     __syncthreads();
     const float s0 = s_sh[4 * c2 + 0], s1 = s_sh[4 * c2 + 1], s2 = s_sh[4 * c2 + 2], s3 = s_sh[4 * c2 + 3];
@@ -882,7 +897,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
                 qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
             }
             __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst, vq,
-                                                  (uint32_t)(cc * k_pad + 1024 * i), 0);
+                                                  (uint32_t)(cc * k_pad + 1024 * i), kWT ? 16 /* sc1 */ : 0);
         }
     }
 }

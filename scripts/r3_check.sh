@@ -24,6 +24,7 @@ for s in ${STEPS:-pytest pplab bench}; do
     f4)     run f4 300 lab/build/w4_lab 4096 4096 4096 9 pp2,pp2_nostore,f4,f4_nostore,f4rm,f4_noload_ns ;;
     w4big)  run w4big 300 lab/build/w4_lab 8192 4096 4096 5 pp2,w4 ;;
     w4clock) run w4clock 300 lab/build/w4_lab 4096 4096 4096 0 clock ;;
+    fused)  run fused 240 lab/build/fused_lab 7 ;;
     pmc)    CFG=${CFG:-c2} run pmc 900 bash scripts/pmc_bench.sh ;;
     bench)  run bench 600 python bench.py --steps 200 --warmup 50 --no-cpu-baseline --node-reps 0 --cold-steps 0 ;;
     benchfull) run benchfull 600 python bench.py ;;
