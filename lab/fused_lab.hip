@@ -110,7 +110,7 @@ __global__ __launch_bounds__(512, 2) void fused_kernel(Fused f) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    pp_tile_body<2>(f.g, lds, tile, 0, 1);
+    pp_tile_body<2, kEpiNone, kPPLayoutF>(f.g, lds, tile, 0, 1);
 }
 
 int main(int argc, char **argv) {
@@ -132,7 +132,7 @@ int main(int argc, char **argv) {
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     auto serial = [&] {
         CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s, 0));
-        gemm_i8_pp<2><<<g.tiles_m * g.tiles_n, kThreads, 0, s>>>(g);
+        gemm_i8_pp<2, kEpiNone, kPPLayoutF><<<g.tiles_m * g.tiles_n, kThreads, 0, s>>>(g);
     };
     const int nblocks = n / 8 + m / 8 + (m / 256) * (n / 256);
     auto fused = [&](int order) {

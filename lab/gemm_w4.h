@@ -35,20 +35,10 @@ enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4Pad
 __device__ unsigned long long g_w4_stamp[4096 * 6];
 #endif
 
-// one MFMA, accumulator pinned to its AGPR quad
-__device__ __forceinline__ void mfma_agpr(v4i &acc, const v4i &a, const v4i &b) {
-    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
+// mfma_agpr (one MFMA, accumulator pinned to its AGPR quad) and uniform_ptr come from gemm_i8_kernels.h
 
 constexpr int kW4Threads = 256;
 
-// a pointer the compiler can PROVE wave-uniform (cdna_hip_programming.md T20: a buffer descriptor built
-// from anything it cannot prove uniform gets a waterfall loop around every buffer op)
-__device__ __forceinline__ const int8_t *uniform_ptr(const int8_t *q) {
-    const uint64_t v = reinterpret_cast<uint64_t>(q);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return reinterpret_cast<const int8_t *>(((uint64_t)hi << 32) | lo);
-}
 constexpr int kW4TStride = 260;  // padded fp32 row of the epilogue image (conflict-free ds_write_b32)
 
 template <int kFlags = kW4PadT>

@@ -62,6 +62,8 @@ int main(int argc, char **argv) {
         {"f4", gemm_i8_f4<0>, 256, true},
         {"f4_nostore", gemm_i8_f4<kW4NoStore>, 256, true},
         {"f4rm", gemm_i8_f4<kW4RowMajor>, 256, false},
+        {"ppF", gemm_i8_pp<2, kEpiNone, kPPLayoutF>, 512, true},
+        {"ppF_nostore", gemm_i8_pp<2, kEpiNone, kPPLayoutF | kPPNoStore>, 512, true},
         {"f4_noload_ns", gemm_i8_f4<kW4NoStore | kW4NoRead>, 256, true},
     };
     dim3 grid(p.tiles_m * p.tiles_n);
@@ -79,6 +81,7 @@ int main(int argc, char **argv) {
             {"w4s_nostore", gemm_i8_w4s<kW4Stamp | kW4NoStore>, 256, w4_sym},
             {"f4", gemm_i8_f4<kW4Stamp>, 256, w4_sym},
             {"f4_nostore", gemm_i8_f4<kW4Stamp | kW4NoStore>, 256, w4_sym},
+            {"ppF", gemm_i8_pp<2, kEpiNone, kPPStamp | kPPLayoutF>, 512, pp_sym},
         };
         const int nb = p.tiles_m * p.tiles_n;
         for (auto &v : sv) {
@@ -86,7 +89,8 @@ int main(int argc, char **argv) {
             int launches = 0; float ms = 0;
             CK(hipEventRecord(a));
             while (ms < 2000) {
-                for (int i = 0; i < 200; ++i) v.fn<<<grid, v.threads>>>(strncmp(v.name, "f4", 2) == 0 ? pf : p);
+                for (int i = 0; i < 200; ++i)
+                    v.fn<<<grid, v.threads>>>(strncmp(v.name, "f4", 2) == 0 || strncmp(v.name, "ppF", 3) == 0 ? pf : p);
                 launches += 200;
                 CK(hipEventRecord(z)); CK(hipEventSynchronize(z)); CK(hipEventElapsedTime(&ms, a, z));
             }

@@ -345,12 +345,20 @@ class Packed:
         return self.buf[: 4 * self.rows_pad].view(torch.float32)
 
     @property
-    def q(self):
-        """X_int8 (rows_pad x k_pad) or W_int8^T (n_pad x k_pad), zero padded."""
+    def q_raw(self):
+        """The packed bytes as stored: FRAGMENT-MAJOR (csrc/qgemm_internal.h fofs) -- 1-KiB blocks of 16
+        rows x 64 k in MFMA lane order, block (rg, kb) at (rg * k_pad / 64 + kb) * 1024."""
         import torch
         parts = -(-(self.k - 1) // 256) if self.k > 1 else 1
         off = _round_up(4 * self.rows_pad * (1 + parts), 256)
-        return self.buf[off: off + self.rows_pad * self.k_pad].view(torch.int8).view(self.rows_pad, self.k_pad)
+        return self.buf[off: off + self.rows_pad * self.k_pad].view(torch.int8)
+
+    @property
+    def q(self):
+        """X_int8 (rows_pad x k_pad) or W_int8^T (n_pad x k_pad), zero padded, row-major (a copy, un-permuted
+        from the fragment-major storage: [rg][kb][kc][r][16 B] -> [rg][r][kb][kc][16 B])."""
+        r16, kb = self.rows_pad // 16, self.k_pad // 64
+        return (self.q_raw.view(r16, kb, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(self.rows_pad, self.k_pad))
 
 
 def _alloc_packed(rows, k, device):

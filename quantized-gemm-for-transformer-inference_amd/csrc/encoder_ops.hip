@@ -110,8 +110,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
     };
     stamp(0);
     if (kPack && row >= rows && row < rows_pad) {  // padding row of the packed view
-        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
-        for (int64_t c = lane; c < k_pad / 4; c += 64) qrow[c] = 0u;
+        auto qrow = [&](int64_t c) __attribute__((always_inline)) -> uint32_t & { return *qword(q, row, 4 * c, k_pad); };  // fragment-major q
+        for (int64_t c = lane; c < k_pad / 4; c += 64) qrow(c) = 0u;
         if (lane == 0) qscale[row] = 0.0f;
         return;
     }
@@ -154,12 +154,12 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
         __builtin_amdgcn_wave_barrier();
         const float cx = absmax_finish(st[0], cand);
         const float sc = inv_divide(range, cx);
-        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+        auto qrow = [&](int64_t c) __attribute__((always_inline)) -> uint32_t & { return *qword(q, row, 4 * c, k_pad); };  // fragment-major q
         for (int c4 = lane; c4 < (int)(k_pad / 4); c4 += 64) {
             int qb[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) qb[e] = 4 * c4 + e < w ? quant_i8(st[4 * c4 + e], sc) : 0;
-            qrow[c4] = (uint32_t)(qb[0] & 0xff) | ((uint32_t)(qb[1] & 0xff) << 8) | ((uint32_t)(qb[2] & 0xff) << 16) |
+            qrow(c4) = (uint32_t)(qb[0] & 0xff) | ((uint32_t)(qb[1] & 0xff) << 8) | ((uint32_t)(qb[2] & 0xff) << 16) |
                        ((uint32_t)(qb[3] & 0xff) << 24);
         }
         if (lane == 0) qscale[row] = cx;
@@ -184,8 +184,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     };
     stamp(0);
     if (kPack && row >= rows && row < rows_pad) {  // padding row of the packed view
-        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
-        for (int64_t c = lane; c < k_pad / 4; c += 64) qrow[c] = 0u;
+        auto qrow = [&](int64_t c) __attribute__((always_inline)) -> uint32_t & { return *qword(q, row, 4 * c, k_pad); };  // fragment-major q
+        for (int64_t c = lane; c < k_pad / 4; c += 64) qrow(c) = 0u;
         if (lane == 0) qscale[row] = 0.0f;
         return;
     }
@@ -253,15 +253,15 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
         const float seed = __shfl(x[0].x, 0, 64);  // column 0: lane 0, i = 0
         const float cx = absmax_finish(seed, cand);
         const float sc = inv_divide(range, cx);
-        uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+        auto qrow = [&](int64_t c) __attribute__((always_inline)) -> uint32_t & { return *qword(q, row, 4 * c, k_pad); };  // fragment-major q
 #pragma unroll
         for (int i = 0; i < kV; ++i) {
             const int j = lane + 64 * i;
             if (j < w4)
-                qrow[j] = (uint32_t)(quant_i8(x[i].x, sc) & 0xff) | ((uint32_t)(quant_i8(x[i].y, sc) & 0xff) << 8) |
+                qrow(j) = (uint32_t)(quant_i8(x[i].x, sc) & 0xff) | ((uint32_t)(quant_i8(x[i].y, sc) & 0xff) << 8) |
                           ((uint32_t)(quant_i8(x[i].z, sc) & 0xff) << 16) | ((uint32_t)(quant_i8(x[i].w, sc) & 0xff) << 24);
         }
-        for (int64_t c4 = w4 + lane; c4 < k_pad / 4; c4 += 64) qrow[c4] = 0u;  // padding columns
+        for (int64_t c4 = w4 + lane; c4 < k_pad / 4; c4 += 64) qrow(c4) = 0u;  // padding columns
         if (lane == 0) qscale[row] = cx;
     }
     stamp(6);

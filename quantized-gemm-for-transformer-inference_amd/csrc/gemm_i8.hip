@@ -13,7 +13,7 @@ namespace qgemm {
 
 using namespace gemm;
 
-const char *gemm_config_name() { return "i8mfma16x16x64_t256x256x128_w8_pingpong_glds2_ldsepi"; }
+const char *gemm_config_name() { return "i8mfma16x16x64_t256x256_w4_wt128x128_fragmajor_direct_agpr"; }
 
 static thread_local GemmEvents t_events;
 static int g_event_mode = 0;  // 0: hipExtLaunchKernel events, 1: hipEventRecord around the launch
@@ -101,20 +101,29 @@ __global__ __launch_bounds__(256) void zero_tickets_kernel(unsigned *__restrict_
     if (i < n) t[i] = 0u;
 }
 
-// 256 x 256 tiles: the ping-pong schedule (gemm_i8_pp<2>: race-free staging; mode 1 measured lab/pp_lab.hip at 4096^3: 62.8 vs 64.2 us for
-// gemm_i8_v3; 8192x4096x4096 123.9 vs 127.9; 2048x16384x4096 122.1 vs 129.3; bit-identical)
-template <int kEpi>
-static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
+// 256 x 256 tiles: gemm_i8_fm (4 waves of 128 x 128, operands straight from the fragment-major packed
+// layout, no LDS in the main loop) where the tile is not split; the ping-pong kernel (gemm_i8_pp<2>, on the
+// same layout) for split-K plans and the LLM.int8() outlier epilogue, which it implements.
+template <typename Launch>
+static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const GemmArgs &p, Launch kernel) {
     const GemmEvents ev = take_gemm_events();
     if ((ev.start || ev.stop) && g_event_mode == 0) {
-        hipExtLaunchKernelGGL((gemm_i8_pp<2, kEpi>), grid, dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p);
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, ev.start, ev.stop, 0, p);
         return hipGetLastError();
     }
     if (ev.start) (void)hipEventRecord(ev.start, stream);
-    gemm_i8_pp<2, kEpi><<<grid, dim3(kThreads), 0, stream>>>(p);
+    kernel<<<grid, block, 0, stream>>>(p);
     hipError_t e = hipGetLastError();
     if (ev.stop) (void)hipEventRecord(ev.stop, stream);
     return e;
+}
+
+template <int kEpi>
+static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
+    if (p.splits > 1 || kEpi == kEpiOutlier)
+        return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF>);
+    if constexpr (kEpi != kEpiOutlier) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);
+    return hipErrorNotSupported;
 }
 
 template <int TB, int kEpi, int kDepth>
@@ -192,7 +201,7 @@ hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Ac
     if (!shape_ok(a, b)) return hipErrorInvalidValue;
     GemmArgs p{a.q, b.q, a.scale, b.scale, Acc, n, 1, m, n, a.k_pad, (int)(a.rows_pad / BM), (int)(b.rows_pad / BN),
                0.0f, 1, nullptr, nullptr, nullptr, 0};
-    gemm_i8_v1<kStoreDirect, false><<<dim3(p.tiles_m * p.tiles_n), dim3(kThreads), 0, stream>>>(p);
+    gemm_i8_fm<kEpiNone, true><<<dim3(p.tiles_m * p.tiles_n), dim3(kFmThreads), 0, stream>>>(p);
     return hipGetLastError();
 }
 

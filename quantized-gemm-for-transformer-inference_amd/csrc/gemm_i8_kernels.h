@@ -707,7 +707,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_v3(GemmArgs p) {
 // into a slot comes after the barrier that follows the last reads of it (lgkmcnt(0) before each
 // R-slot barrier).  Barrier counts match: lead 1 + 2nk, lag 2 + 2nk - 1.
 // lab-only flags (kPP*): in-kernel stamps, ablations
-enum PPFlags { kPPStamp = 1, kPPNoDma = 2, kPPNoStore = 4, kPPNtStore = 8 };
+// kPPLayoutF: operands in the FRAGMENT-MAJOR packed layout (1-KiB blocks of 16 rows x 64 k in MFMA lane
+// order, block (rg, kb) at ((rg * (k_pad / 64)) + kb) * 1024): every LDS-DMA piece is one contiguous block,
+// the LDS image is block order, and a fragment read is one contiguous 1 KiB (no swizzle needed)
+enum PPFlags { kPPStamp = 1, kPPNoDma = 2, kPPNoStore = 4, kPPNtStore = 8, kPPLayoutF = 16 };
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_pp_stamp[4096 * 6];
 #endif
@@ -731,7 +734,7 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
             }
     };
 #else
-    static_assert((kFlags & ~kPPNtStore) == 0, "lab flags need QGEMM_LAB");
+    static_assert((kFlags & ~(kPPNtStore | kPPLayoutF)) == 0, "lab flags need QGEMM_LAB");
     auto stamp = [](int) {};
 #endif
     stamp(0);
@@ -745,28 +748,37 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
     const int kt0 = slice * nk_all / S;
     const int nk = (slice + 1) * nk_all / S - kt0;
     const int64_t kp = p.k_pad;
-    const int8_t *Ablk = p.A + (int64_t)tm * BM * kp + (int64_t)kt0 * BK;
-    const int8_t *Bblk = p.B + (int64_t)tn * BN * kp + (int64_t)kt0 * BK;
+    constexpr bool kF = (kFlags & kPPLayoutF) != 0;
+    const int64_t nkg = kp / 64;  // F-layout: 1-KiB blocks per 16-row group
+    const int8_t *Ablk = kF ? p.A + ((int64_t)tm * 16 * nkg + (int64_t)kt0 * 2) * 1024
+                            : p.A + (int64_t)tm * BM * kp + (int64_t)kt0 * BK;
+    const int8_t *Bblk = kF ? p.B + ((int64_t)tn * 16 * nkg + (int64_t)kt0 * 2) * 1024
+                            : p.B + (int64_t)tn * BN * kp + (int64_t)kt0 * BK;
     // piece q (8 rows x 128 B, one wave instruction) of an operand: lane l writes LDS bytes 16l.. of
-    // rows 8q.., i.e. row 8q + (l>>3), slot l&7, which holds global chunk (l&7) ^ (4(q&1) + (l>>4))
+    // rows 8q.., i.e. row 8q + (l>>3), slot l&7, which holds global chunk (l&7) ^ (4(q&1) + (l>>4)).
+    // F-layout: piece q = block (row group q >> 1, k-block q & 1) of the k-step, copied whole
     uint32_t voff[2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) voff[e] = (uint32_t)((lane >> 3) * kp) + ((((lane & 7) ^ (4 * e + (lane >> 4)))) << 4);
+    for (int e = 0; e < 2; ++e)
+        voff[e] = kF ? (uint32_t)(lane * 16)
+                     : (uint32_t)((lane >> 3) * kp) + ((((lane & 7) ^ (4 * e + (lane >> 4)))) << 4);
+    auto piece_src = [&](const int8_t *blk, int q, int kt) __attribute__((always_inline)) -> const int8_t * {
+        if constexpr (kF) return blk + ((int64_t)(q >> 1) * nkg + (int64_t)kt * 2 + (q & 1)) * 1024 + voff[0];
+        else return blk + (int64_t)q * 8 * kp + (int64_t)kt * BK + voff[q & 1];
+    };
     // wave-uniform part: 8 pieces starting at piece q0 of one operand, k-step kt, into LDS at dst
     auto pieces8 = [&](const int8_t *blk, int q0, int kt, int8_t *dst) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int q = q0 + i;
-            __builtin_amdgcn_global_load_lds((const void *)(blk + (int64_t)q * 8 * kp + (int64_t)kt * BK + voff[i & 1]),
-                                             (void *)(dst + q * 8 * BK), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)piece_src(blk, q, kt), (void *)(dst + q * 8 * BK), 16, 0, 0);
         }
     };
     auto pieces4 = [&](const int8_t *blk, int q0, int kt, int8_t *dst) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int q = q0 + i;  // q0 even: piece parity = i & 1
-            __builtin_amdgcn_global_load_lds((const void *)(blk + (int64_t)q * 8 * kp + (int64_t)kt * BK + voff[i & 1]),
-                                             (void *)(dst + q * 8 * BK), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)piece_src(blk, q, kt), (void *)(dst + q * 8 * BK), 16, 0, 0);
         }
     };
     // mode 2: this wave's A rows (its half: lead rows 0-127, lag rows 128-255) / its B half-strip
@@ -784,10 +796,12 @@ __device__ __forceinline__ void pp_tile_body(const GemmArgs &p, int8_t *lds, int
     };
 
     const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
-    const int a_row0 = (wm * 128 + lrow) * BK, b_row0 = (wn * 64 + lrow) * BK;
+    // F-layout image: fragment (row block, sub-step s) = block ((rows >> 4), s) = lane's 16 B at lane * 16
+    const int a_row0 = kF ? wm * 128 * BK + lane * 16 : (wm * 128 + lrow) * BK;
+    const int b_row0 = kF ? wn * 64 * BK + lane * 16 : (wn * 64 + lrow) * BK;
     int off[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+    for (int s = 0; s < 2; ++s) off[s] = kF ? s * 1024 : ((4 * s + kq) ^ swz) << 4;
 
     v4i acc[8][4];
 #pragma unroll
@@ -957,6 +971,178 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_i8_pp(GemmArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// gemm_i8_fm: the product 256 x 256 tile (round 3).  4 waves (one per SIMD), each a 128 x 128 wave tile =
+// 8 x 8 v_mfma_i32_16x16x64_i8 accumulators (256 registers, pinned in AGPRs: every MFMA is an inline-asm
+// statement with its accumulator as a tied "+a" operand -- hipcc's builtin form kept them in AGPRs but
+// moved them around the loop, lab gemm_variants.h v9), operands streamed from the FRAGMENT-MAJOR packed
+// layout (qgemm_internal.h fofs) straight into VGPRs: one MFMA operand = one contiguous 1-KiB
+// buffer_load_dwordx4.  No LDS and no barrier in the main loop: three register sets, sub-step u computes
+// while u+1 and u+2 are in flight (hipcc's counted vmcnt waits).  The two waves that share an A (B) half
+// read the same blocks (L1).  Measured against the ping-pong kernel (lab/w4_lab.hip, 4096^3, 5 boxes, bit-
+// identical): 58.3-62.3 vs 62.7-64.9 us; its main loop holds 1.90-1.97 GHz (no LDS traffic) vs 1.77-1.83.
+// Epilogue: per wave, two steps of 64 rows of its quadrant dequantized (scales in registers) into its OWN
+// padded [64][132] LDS block and stored from there as 512-B row segments: no cross-wave hand-off.
+// kI32: the raw int32 accumulators (qgemm_mm_packed_i32) instead of the dequantized fp32.
+__device__ __forceinline__ void mfma_agpr(v4i &acc, const v4i &a, const v4i &b) {
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// a pointer the compiler can PROVE wave-uniform (cdna_hip_programming.md T20: a buffer descriptor built
+// from anything it cannot prove uniform gets a waterfall loop around every buffer op)
+__device__ __forceinline__ const int8_t *uniform_ptr(const int8_t *q) {
+    const uint64_t v = reinterpret_cast<uint64_t>(q);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const int8_t *>(((uint64_t)hi << 32) | lo);
+}
+
+constexpr int kFmThreads = 256;
+
+template <int kEpi = kEpiNone, bool kI32 = false>
+__global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
+    static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
+    constexpr int TS = 132;                 // padded row of a wave's epilogue block (conflict-free ds_write)
+    constexpr int kBlockBytes = 64 * TS * 4;
+    __shared__ __attribute__((aligned(16))) int8_t lds[4 * kBlockBytes + 2048];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int tm, tn;
+    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    const int nsub = (int)(p.k_pad / 64);
+    // this wave's half panels: 8 row groups x nsub blocks each (= 128 packed rows)
+    const int half_bytes = 8 * nsub * 1024;
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int8_t *>(uniform_ptr(p.A + ((int64_t)tm * 16 + wm * 8) * nsub * 1024)), 0,
+        __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
+    const auto rsB = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int8_t *>(uniform_ptr(p.B + ((int64_t)tn * 16 + wn * 8) * nsub * 1024)), 0,
+        __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
+    const int voff = lane * 16;
+
+    v4i acc[8][8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = v4i{};
+    v4i a0[8], b0[8], a1[8], b1[8], a2[8], b2[8];
+    // fragment loads of sub-step u: j < 8 -> B block (row group j of the half, k-block u), else A
+    auto ld = [&](v4i (&fa)[8], v4i (&fb)[8], int j, int u) __attribute__((always_inline)) {
+        const int soff = ((j & 7) * nsub + u) * 1024;
+        if (j < 8) fb[j] = __builtin_amdgcn_raw_buffer_load_b128(rsB, voff, soff, 0);
+        else fa[j - 8] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voff, soff, 0);
+    };
+    // MFMAs on (ca, cb), loads of sub-step un into (na, nb); in the main loop the loads are unconditional
+    // (index clamped to the last sub-step: a conditional register load makes hipcc keep both values alive
+    // across the loop and spill a register set)
+    auto substep = [&](v4i (&ca)[8], v4i (&cb)[8], v4i (&na)[8], v4i (&nb)[8], int un, bool more)
+                       __attribute__((always_inline)) {
+        un = un < nsub ? un : nsub - 1;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni) mfma_agpr(acc[mi][ni], ca[mi], cb[ni]);
+            if (more) {
+                ld(na, nb, 2 * mi, un);
+                ld(na, nb, 2 * mi + 1, un);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+    };
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ld(a0, b0, j, 0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ld(a1, b1, j, nsub > 1 ? 1 : 0);
+    int u = 0;
+    for (; u + 3 <= nsub; u += 3) {
+        substep(a0, b0, a2, b2, u + 2, true);
+        substep(a1, b1, a0, b0, u + 3, true);
+        substep(a2, b2, a1, b1, u + 4, true);
+    }
+    const int rest = nsub - u;  // 0, 1 or 2: sets 0 and 1 hold sub-steps u, u+1
+    if (rest > 0) {
+        substep(a0, b0, a2, b2, 0, false);
+        if (rest > 1) substep(a1, b1, a2, b2, 0, false);
+    }
+    // the last MFMAs' results are read by VALU below; the asm statements hide them from hipcc's padding
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+    const int gi0 = tm * BM, gj0 = tn * BN;
+    const int lrow = lane & 15, kq = lane >> 4;
+    const int r0 = wm * 128, c0 = wn * 128;
+    float *sCx = reinterpret_cast<float *>(lds + 4 * kBlockBytes);
+    float *sCw = sCx + BM;
+    if constexpr (!kI32) {
+        sCx[tid] = p.Cx[gi0 + tid];  // scales are padded to the 256-row tiles
+        sCw[tid] = p.Cw[gj0 + tid];
+    }
+    __syncthreads();
+    float *T = reinterpret_cast<float *>(lds + wave * kBlockBytes);
+    const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
+                      gj0 + BN <= p.n && gi0 + BM <= p.m;
+    // the scales (and bias) into registers first: T and the scales share the one LDS array, so a scale read
+    // between T stores would be re-issued and waited for after every store
+    float cwv[8], bv[8];
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+        cwv[ni] = kI32 ? 0.0f : sCw[c0 + ni * 16 + lrow];
+        const int j = gj0 + c0 + ni * 16 + lrow;
+        bv[ni] = has_bias(kEpi) && j < p.n ? p.bias[j] : 0.0f;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        float cxv[4][4];
+#pragma unroll
+        for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cxv[mq][r] = kI32 ? 0.0f : sCx[r0 + 64 * s + mq * 16 + 4 * kq + r];
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+            const int jl = ni * 16 + lrow;
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int il = mq * 16 + 4 * kq + r;
+                    float o;
+                    if constexpr (kI32) {
+                        o = __int_as_float(acc[4 * s + mq][ni][r]);  // the raw bits travel through LDS
+                    } else {
+                        o = dequantize(acc[4 * s + mq][ni][r], outer_product(cxv[mq][r], cwv[ni]), p.inv_r2);
+                        if constexpr (has_bias(kEpi)) o = __fadd_rn(o, bv[ni]);
+                        if constexpr (kEpi == kEpiBiasRelu) o = (o < 0.0f) ? 0.0f : o;
+                    }
+                    T[il * TS + jl] = o;
+                }
+        }
+        // the wave's own block: its ds_writes precede its ds_reads (one wave's LDS ops stay in order)
+        const int c4 = (lane & 31) * 4;
+        float *C = static_cast<float *>(p.C);
+        if (full) {
+#pragma unroll 8
+            for (int it = 0; it < 32; ++it) {
+                const int rr = 2 * it + (lane >> 5);
+                const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
+                *reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4) = v;
+            }
+        } else {
+            for (int it = 0; it < 32; ++it) {
+                const int rr = 2 * it + (lane >> 5);
+                const int i = gi0 + r0 + 64 * s + rr;
+                const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
+                const int j = gj0 + c0 + c4;
+                if (i >= p.m) continue;
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // gemm_i8_small<TB>: TB x TB macro-tiles (TB = 128 or 64) for problems with few 256 x 256 tiles (the
 // encoder's M = 512 linears, decode-sized M): 4 waves as 2 x 2, each (TB/2) x (TB/2) = MI x MI tiles
 // of v_mfma_i32_16x16x64_i8, the same staging (LDS-DMA, source-swizzled 128-B rows, 2-deep ring),
@@ -1001,21 +1187,23 @@ __global__ __launch_bounds__((SmallTile<TB, kDepth>::kThreads), (SmallTile<TB, k
     const int nk_all = (int)(p.k_pad / BK);
     const int kt0 = slice * nk_all / S;
     const int nk = (slice + 1) * nk_all / S - kt0;
-    // staging: wave w fills rows [RPW w, RPW w + RPW) of both tiles, 8 rows (1 KiB) per LDS-DMA, chunk g
-    // of row r at slot g ^ ((r>>1)&7)
-    const int8_t *Ablk = p.A + (int64_t)tm * TB * p.k_pad;
+    // staging (fragment-major operands, qgemm_internal.h fofs): a k-step of a TB-row tile is TB/16 row groups
+    // x 2 k-blocks of 1 KiB; wave w copies blocks q = w NP + i (row group q >> 1, k-block q & 1) whole, one
+    // LDS-DMA each, to LDS q * 1 KiB -- the LDS image is block order and a fragment read one contiguous 1 KiB
+    const int8_t *Ablk = p.A + (int64_t)tm * TB * p.k_pad;  // = the tile's first row group (TB % 16 == 0)
     const int8_t *Bblk = p.B + (int64_t)tn * TB * p.k_pad;
+    const int64_t nkg = p.k_pad / 64;
     int64_t src_off[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-        const int row = wave * RPW + i * 8 + (lane >> 3);
-        src_off[i] = (int64_t)row * p.k_pad + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+        const int q = wave * NP + i;
+        src_off[i] = ((int64_t)(q >> 1) * nkg + (q & 1)) * 1024 + lane * 16;
     }
     auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
         int8_t *la = lds + buf * T_::kStageBytes;
         int8_t *lb = la + T_::kTileBytes;
-        const int8_t *ga = Ablk + (int64_t)kt * BK;
-        const int8_t *gb = Bblk + (int64_t)kt * BK;
+        const int8_t *ga = Ablk + (int64_t)kt * 2048;
+        const int8_t *gb = Bblk + (int64_t)kt * 2048;
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
             __builtin_amdgcn_global_load_lds((const void *)(ga + src_off[i]), (void *)(la + (wave * RPW + i * 8) * BK), 16,
@@ -1024,11 +1212,12 @@ __global__ __launch_bounds__((SmallTile<TB, kDepth>::kThreads), (SmallTile<TB, k
                                              0, 0);
         }
     };
-    const int lrow = lane & 15, kq = lane >> 4, swz = (lrow >> 1) & 7;
-    const int a_row0 = (wm * WT + lrow) * BK, b_row0 = (wn * WT + lrow) * BK;
+    const int lrow = lane & 15, kq = lane >> 4;
+    // fragment (16 rows from r, sub-step s) = LDS block ((r >> 4), s): the lane's 16 B at lane * 16
+    const int a_row0 = wm * WT * BK + lane * 16, b_row0 = wn * WT * BK + lane * 16;
     int off[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) off[s] = ((4 * s + kq) ^ swz) << 4;
+    for (int s = 0; s < 2; ++s) off[s] = s * 1024;
 
     v4i acc[MI][MI];
 #pragma unroll

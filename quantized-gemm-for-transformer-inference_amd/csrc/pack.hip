@@ -103,10 +103,11 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     const int lane = threadIdx.x & 63;
     const int64_t row = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     if (row >= rows_pad) return;
-    uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+    // dword c of the packed row (k = 4c), fragment-major layout (qgemm_internal.h fofs)
+    auto qrow = [&](int64_t c) __attribute__((always_inline)) { return qword(q, row, 4 * c, k_pad); };
     const int64_t nq = k_pad >> 2;  // uint32 words per packed row
     if (row >= rows) {              // padding row
-        for (int64_t c = lane; c < nq; c += kWave) st_u32<kWT>(qrow + c, 0u);
+        for (int64_t c = lane; c < nq; c += kWave) st_u32<kWT>(qrow(c), 0u);
         if (lane == 0) st_f32<kWT>(scale + row, 0.0f);
         return;
     }
@@ -201,13 +202,13 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         for (int j = 0; j < R; ++j) {
             const int c = lane + j * kWave;
             if (c < nfull)
-                st_u32<kWT>(qrow + c, pack4(quant_i8(v[j].x, s), quant_i8(v[j].y, s), quant_i8(v[j].z, s),
+                st_u32<kWT>(qrow(c), pack4(quant_i8(v[j].x, s), quant_i8(v[j].y, s), quant_i8(v[j].z, s),
                                             quant_i8(v[j].w, s)));
         }
     } else {
         for (int c = lane; c < nfull; c += kWave) {
             float4 x = s4[c];
-            st_u32<kWT>(qrow + c, pack4(quant_i8(x.x, s), quant_i8(x.y, s), quant_i8(x.z, s), quant_i8(x.w, s)));
+            st_u32<kWT>(qrow(c), pack4(quant_i8(x.x, s), quant_i8(x.y, s), quant_i8(x.z, s), quant_i8(x.w, s)));
         }
     }
     // partial tail word, then zero padding words
@@ -215,9 +216,9 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     if ((len & 3) && lane == 0) {
         int b[4] = {0, 0, 0, 0};
         for (int e = 0; e < (len & 3); ++e) b[e] = quant_i8(srow[tail0 + e], s);
-        st_u32<kWT>(qrow + nfull, pack4(b[0], b[1], b[2], b[3]));
+        st_u32<kWT>(qrow(nfull), pack4(b[0], b[1], b[2], b[3]));
     }
-    for (int64_t c = first_zero + lane; c < nq; c += kWave) st_u32<kWT>(qrow + c, 0u);
+    for (int64_t c = first_zero + lane; c < nq; c += kWave) st_u32<kWT>(qrow(c), 0u);
     if (lane == 0) st_f32<kWT>(scale + row, cx);
 }
 
@@ -231,10 +232,10 @@ __device__ __forceinline__ void pack_row_block_body(int64_t row, const float *__
                                                     float *red) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (row >= rows_pad) return;
-    uint32_t *qrow = reinterpret_cast<uint32_t *>(q + row * k_pad);
+    auto qrow = [&](int64_t c) __attribute__((always_inline)) -> uint32_t & { return *qword(q, row, 4 * c, k_pad); };
     const int64_t nq = k_pad >> 2;
     if (row >= rows) {  // padding row
-        for (int64_t c = t; c < nq; c += 256) qrow[c] = 0u;
+        for (int64_t c = t; c < nq; c += 256) qrow(c) = 0u;
         if (t == 0) scale[row] = 0.0f;
         return;
     }
@@ -271,15 +272,15 @@ __device__ __forceinline__ void pack_row_block_body(int64_t row, const float *__
     for (int j = 0; j < 16; ++j) {
         const int c = t + 256 * j;
         if (c < nfull)
-            qrow[c] = pack4(quant_i8(v[j].x, sc), quant_i8(v[j].y, sc), quant_i8(v[j].z, sc), quant_i8(v[j].w, sc));
+            qrow(c) = pack4(quant_i8(v[j].x, sc), quant_i8(v[j].y, sc), quant_i8(v[j].z, sc), quant_i8(v[j].w, sc));
     }
     const int64_t first_zero = nfull + ((len & 3) ? 1 : 0);
     if ((len & 3) && t == 0) {
         int b[4] = {0, 0, 0, 0};
         for (int e = 0; e < (len & 3); ++e) b[e] = quant_i8(srow[tail0 + e], sc);
-        qrow[nfull] = pack4(b[0], b[1], b[2], b[3]);
+        qrow(nfull) = pack4(b[0], b[1], b[2], b[3]);
     }
-    for (int64_t c = first_zero + t; c < nq; c += 256) qrow[c] = 0u;
+    for (int64_t c = first_zero + t; c < nq; c += 256) qrow(c) = 0u;
     if (t == 0) scale[row] = cx;
 }
 
@@ -307,9 +308,9 @@ __global__ __launch_bounds__(256) void pack_rows_generic_kernel(const float *__r
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows_pad) return;
-    int8_t *qrow = q + row * k_pad;
+    auto qrow = [&](int64_t c) __attribute__((always_inline)) -> int8_t & { return q[fofs(row, c, k_pad)]; };
     if (row >= rows) {
-        for (int64_t c = lane; c < k_pad; c += kWave) qrow[c] = 0;
+        for (int64_t c = lane; c < k_pad; c += kWave) qrow(c) = 0;
         if (lane == 0) scale[row] = 0.0f;
         return;
     }
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256) void pack_rows_generic_kernel(const float *__r
     p = wave_max(p);
     const float cx = absmax_finish(seed, p);
     const float s = inv_divide(range, cx);
-    for (int64_t c = lane; c < k_pad; c += kWave) qrow[c] = (c < len) ? (int8_t)quant_i8(srow[c * sw], s) : 0;
+    for (int64_t c = lane; c < k_pad; c += kWave) qrow(c) = (c < len) ? (int8_t)quant_i8(srow[c * sw], s) : 0;
     if (lane == 0) scale[row] = cx;
 }
 
@@ -497,9 +498,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
         }
         __syncthreads();  // tile tb complete (and, double-buffered, the other one is free to rewrite next)
         const uint32_t *lp = reinterpret_cast<const uint32_t *>(tb + n * kTStride + kc);  // 4-B aligned only
-        uint4 *gp = reinterpret_cast<uint4 *>(q + (n0 + n) * k_pad + k0 + kc);
-        gp[0] = make_uint4(lp[0], lp[1], lp[2], lp[3]);
-        gp[1] = make_uint4(lp[4], lp[5], lp[6], lp[7]);
+        *reinterpret_cast<uint4 *>(q + fofs(n0 + n, k0 + kc, k_pad)) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+        *reinterpret_cast<uint4 *>(q + fofs(n0 + n, k0 + kc + 16, k_pad)) = make_uint4(lp[4], lp[5], lp[6], lp[7]);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -595,8 +595,7 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
         }
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc)
-            *reinterpret_cast<uint32_t *>(q + (n0 + 4 * c4 + cc) * k_pad + r0) =
-                pack4(qv[0][cc], qv[1][cc], qv[2][cc], qv[3][cc]);
+            *qword(q, n0 + 4 * c4 + cc, r0, k_pad) = pack4(qv[0][cc], qv[1][cc], qv[2][cc], qv[3][cc]);
     }
 }
 
@@ -618,8 +617,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
     } else if (bid < nstrips + (int)((w_rows_pad - n) / kWsCols)) {
         // padding rows of packed W: zero rows, zero scales
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kWsCols;
-        for (int64_t i = threadIdx.x; i < (int64_t)kWsCols * k_pad / 16; i += 1024)
-            reinterpret_cast<uint4 *>(w_q + n0 * k_pad)[i] = make_uint4(0, 0, 0, 0);
+        zero_packed_rows(w_q, n0, kWsCols, k_pad, threadIdx.x, 1024);
         if (threadIdx.x < kWsCols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
         // X rows: 16 rows per 1024-thread block = four 4-row groups of the 256-thread body
@@ -726,8 +724,8 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
     }
     __syncthreads();
     const float s0 = s_sh[4 * c8 + 0], s1 = s_sh[4 * c8 + 1], s2 = s_sh[4 * c8 + 2], s3 = s_sh[4 * c8 + 3];
+    // the strip's 32 packed rows = two whole 16-row groups: one contiguous region of the fragment-major q
     const auto dst = buf_rsrc(q + n0 * k_pad, (uint32_t)(kW32Cols * k_pad));
-    const uint32_t vq = (uint32_t)(4 * c8 * k_pad + 4 * rq);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int r0 = 4 * rq + 512 * i;
@@ -744,8 +742,8 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
                 const float sc = cc == 0 ? s0 : cc == 1 ? s1 : cc == 2 ? s2 : s3;
                 qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
             }
-            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst, vq,
-                                                  (uint32_t)(cc * k_pad + 512 * i), 0);
+            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst,
+                                                  (uint32_t)fofs(4 * c8 + cc, r0, k_pad), 0, 0);
         }
     }
 }
@@ -765,8 +763,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
         pack_w_strip32_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kW32Cols;
-        for (int64_t i = threadIdx.x; i < (int64_t)kW32Cols * k_pad / 16; i += 1024)
-            reinterpret_cast<uint4 *>(w_q + n0 * k_pad)[i] = make_uint4(0, 0, 0, 0);
+        zero_packed_rows(w_q, n0, kW32Cols, k_pad, threadIdx.x, 1024);
         if (threadIdx.x < kW32Cols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
         const int64_t xb = bid - nstrips - npad;
@@ -881,8 +878,10 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     __syncthreads();
     const float s0 = s_sh[4 * c2 + 0], s1 = s_sh[4 * c2 + 1], s2 = s_sh[4 * c2 + 2], s3 = s_sh[4 * c2 + 3];
     // 4 consecutive rows of one column = one dword of packed row n0 + 4*c2 + cc
-    const auto dst = buf_rsrc(q + n0 * k_pad, (uint32_t)(kWs8Cols * k_pad));
-    const uint32_t vq = (uint32_t)(4 * c2 * k_pad + 4 * rq);
+    // the strip's 8 packed rows are half of a 16-row group of the fragment-major q: descriptor over the group
+    const int64_t g0 = n0 & ~(int64_t)15;
+    const auto dst = buf_rsrc(q + g0 * k_pad, (uint32_t)(16 * k_pad));
+    const int rr0 = (int)(n0 - g0) + 4 * c2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r0 = 4 * rq + 1024 * i;
@@ -896,8 +895,8 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
                 const float sc = cc == 0 ? s0 : cc == 1 ? s1 : cc == 2 ? s2 : s3;
                 qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
             }
-            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst, vq,
-                                                  (uint32_t)(cc * k_pad + 1024 * i), kWT ? 16 /* sc1 */ : 0);
+            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst,
+                                                  (uint32_t)fofs(rr0 + cc, r0, k_pad), 0, kWT ? 16 /* sc1 */ : 0);
         }
     }
 }
@@ -919,8 +918,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         pack_w_strip8_body<kMask>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kWs8Cols;
-        for (int64_t i = threadIdx.x; i < (int64_t)kWs8Cols * k_pad / 16; i += 512)
-            reinterpret_cast<uint4 *>(w_q + n0 * k_pad)[i] = make_uint4(0, 0, 0, 0);
+        zero_packed_rows(w_q, n0, kWs8Cols, k_pad, threadIdx.x, 512);
         if (threadIdx.x < kWs8Cols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
         const int64_t xb = bid - nstrips - npad;  // rows 8xb + (t>>6): two 4-row groups of the 256-thread body

@@ -18,8 +18,18 @@ constexpr int kColChunk = 256;
 __host__ __device__ inline int64_t colmax_parts(int64_t k) { return k > 1 ? (k - 1 + kColChunk - 1) / kColChunk : 1; }
 
 // Layout of one packed operand buffer:
-//   [scale: rows_pad f32][scratch: parts x rows_pad u32][q: rows_pad x k_pad i8]
+//   [scale: rows_pad f32][scratch: parts x rows_pad u32][q: rows_pad x k_pad i8, FRAGMENT-MAJOR]
 // The scratch holds pack_cols' column-absmax partials (pass 1 -> pass 2).
+//
+// q is stored fragment-major: 1-KiB blocks of 16 packed rows x 64 k-bytes, block (rg, kb) at byte
+// (rg * (k_pad / 64) + kb) * 1024, and inside a block the bytes in the lane order of one
+// v_mfma_i32_16x16x64_i8 operand: lane l = 16 kc + r holds row 16 rg + r, k = 64 kb + 16 kc .. +15.  So a
+// GEMM wave loads a whole MFMA fragment as ONE contiguous 1-KiB buffer_load_dwordx4 (gemm_i8_f4), and
+// an LDS-DMA piece is one block (no source swizzle, conflict-free fragment reads).  Any 4-byte group
+// k .. k+3 with k % 4 == 0 (and any aligned 16-byte group) of one row stays contiguous.
+__host__ __device__ inline int64_t fofs(int64_t row, int64_t k, int64_t k_pad) {
+    return ((row >> 4) * (k_pad >> 6) + (k >> 6)) * 1024 + ((((k >> 4) & 3) << 4) + (row & 15)) * 16 + (k & 15);
+}
 struct PackedView {
     float *scale;       // rows_pad floats (Cx or Cw)
     uint32_t *scratch;  // parts x rows_pad words
@@ -42,6 +52,17 @@ inline PackedView packed_view(const void *base, int rows, int k) {
 inline size_t packed_bytes(int rows, int k) {
     const int64_t rp = round_up(rows, kRowPad);
     return (size_t)round_up(rp * 4 * (1 + colmax_parts(k)), 256) + (size_t)rp * round_up(k, kKPad);
+}
+
+// the dword of packed row `row` holding k .. k+3 (k % 4 == 0)
+__device__ __forceinline__ uint32_t *qword(int8_t *q, int64_t row, int64_t k, int64_t k_pad) {
+    return reinterpret_cast<uint32_t *>(q + fofs(row, k, k_pad));
+}
+// zero packed rows [r0, r0 + nrows) over all k_pad bytes, 16 B per thread-step (threads t of nt)
+__device__ __forceinline__ void zero_packed_rows(int8_t *q, int64_t r0, int nrows, int64_t k_pad, int t, int nt) {
+    const int64_t per = k_pad >> 4;
+    for (int64_t i = t; i < (int64_t)nrows * per; i += nt)
+        *reinterpret_cast<uint4 *>(q + fofs(r0 + i / per, (i % per) << 4, k_pad)) = make_uint4(0, 0, 0, 0);
 }
 
 // ---- the reference's per-element arithmetic, pinned to single IEEE operations ----------------

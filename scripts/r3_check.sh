@@ -21,7 +21,7 @@ for s in ${STEPS:-pytest pplab bench}; do
     pplab8) run pplab8 240 lab/build/pp_lab 8192 4096 4096 5 pp1,pp2 ;;
     ppclock) run ppclock 240 lab/build/pp_lab 4096 4096 4096 0 clock ;;
     w4)     run w4 300 lab/build/w4_lab 4096 4096 4096 7 ;;
-    f4)     run f4 300 lab/build/w4_lab 4096 4096 4096 9 pp2,pp2_nostore,f4,f4_nostore,f4rm,f4_noload_ns ;;
+    f4)     run f4 300 lab/build/w4_lab 4096 4096 4096 9 pp2,pp2_nostore,f4,f4_nostore,ppF,ppF_nostore ;;
     w4big)  run w4big 300 lab/build/w4_lab 8192 4096 4096 5 pp2,w4 ;;
     w4clock) run w4clock 300 lab/build/w4_lab 4096 4096 4096 0 clock ;;
     fused)  run fused 240 lab/build/fused_lab 7 ;;
