@@ -21,6 +21,7 @@ Extra objects on that line:
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -336,6 +337,16 @@ def c4_node(args, qg, dev, world, rank, distributed):
     }
 
 
+def gemm_kernel_name(L, M, N, K, outlier):
+    """The GEMM kernel this call launches, as the library plans it (qgemm_gemm_plan)."""
+    if outlier:
+        return ("gemm_i8_pp<2, kEpiOutlier> (256x256 tiles, 8 waves ping-pong, LDS-DMA ring, fused dequant + "
+                "outlier fp32 chain)")
+    tile, name = ctypes.c_int(0), ctypes.c_char_p()
+    splits = L.qgemm_gemm_plan(M, N, K, ctypes.byref(tile), ctypes.byref(name))
+    return f"{name.value.decode()}, plan: {tile.value}-tiles x {splits} K-slice(s)"
+
+
 def main():
     args = parse()
     import torch
@@ -468,8 +479,7 @@ def main():
             "traffic_unit": "bytes per launch (HBM + Infinity Cache fill, FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
             "alg_bytes": M * K + N * K + 4 * M * N + 4 * (M + N),
-            "kernel": "gemm_i8_pp<2> (int8 16x16x64 MFMA GEMM, ping-pong schedule, fused dequant epilogue"
-                      + (" + outlier fp32 chain)" if outlier else ")"),
+            "kernel": gemm_kernel_name(L, M, N, K, outlier),
             "ceiling_measured": {
                 "value": PRACTICAL_INT8_TOPS, "frac": round(achieved / PRACTICAL_INT8_TOPS, 4),
                 "note": "bare v_mfma_i32_16x16x64_i8 issue, operands in registers, no VALU in the loop, every CU, "

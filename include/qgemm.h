@@ -162,6 +162,11 @@ QGEMM_API int qgemm_set_gemm_events(void *start_event, void *stop_event);
  * stream right before / after the GEMM launch. */
 QGEMM_API int qgemm_set_event_mode(int mode);
 
+/* Diagnostics: the int8 GEMM launch plan op_mm_quantize* / qgemm_mm_packed use for an m x n x k call:
+ * returns the number of K slices (1 = no split-K; < 0 on invalid sizes) and, when non-NULL, the
+ * macro-tile edge (256, 64 or 32) and a static string naming the kernel. */
+QGEMM_API int qgemm_gemm_plan(int m, int n, int k, int *tile, const char **kernel);
+
 /* Library identification: "qgemm <version> gfx950 <kernel config>". */
 QGEMM_API const char *qgemm_version(void);
 

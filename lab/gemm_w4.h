@@ -29,7 +29,8 @@
 namespace qgemm {
 namespace gemm {
 
-enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4PadT = 16, kW4RowMajor = 32 };
+enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4PadT = 16, kW4RowMajor = 32, kW4NoA = 64,
+               kW4NoB = 128, kW4K1 = 256, kW4K4 = 512, kW4Sync = 1024 };
 
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_w4_stamp[4096 * 6];
@@ -498,10 +499,13 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
         for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = v4i{};
     v4i a0[8], b0[8], a1[8], b1[8], a2[8], b2[8];
     // fragment loads of sub-step u: j < 8 -> B block j, else A block j - 8
-    auto ld = [&](v4i (&fa)[8], v4i (&fb)[8], int j, int u) __attribute__((always_inline)) {
+    auto ld = [&](v4i (&fa)[8], v4i (&fb)[8], int j, int u, bool pro = false) __attribute__((always_inline)) {
         const int soff = kRM ? ((j & 7) * 16 * nsub * 64 + u * 64) : (((j & 7) * nsub + u) * 1024);
-        if (j < 8) fb[j] = __builtin_amdgcn_raw_buffer_load_b128(rsB, voff, soff, 0);
-        else fa[j - 8] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voff, soff, 0);
+        if (j < 8) {
+            if (!(kFlags & kW4NoB) || pro) fb[j] = __builtin_amdgcn_raw_buffer_load_b128(rsB, voff, soff, 0);
+        } else if (!(kFlags & kW4NoA) || pro) {
+            fa[j - 8] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voff, soff, 0);
+        }
     };
     // MFMAs on (ca, cb); loads of sub-step un into (na, nb) when `more`.  In the main loop the loads are
     // unconditional (the sub-step index clamped to the last one): a conditional register load makes hipcc
@@ -509,6 +513,8 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
     auto substep = [&](v4i (&ca)[8], v4i (&cb)[8], v4i (&na)[8], v4i (&nb)[8], int un, bool more)
                        __attribute__((always_inline)) {
         un = un < nsub ? un : nsub - 1;
+        if constexpr (kFlags & kW4K1) un = 0;   // ablation: every load re-reads sub-step 0 (L1 / L2 hits)
+        if constexpr (kFlags & kW4K4) un &= 3;  // ablation: 4 sub-steps cycled (L2 hits)
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi) {
@@ -523,12 +529,17 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
         __builtin_amdgcn_s_setprio(0);
     };
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ld(a0, b0, j, 0);
+    for (int j = 0; j < 16; ++j) ld(a0, b0, j, 0, true);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ld(a1, b1, j, nsub > 1 ? 1 : 0);
+    for (int j = 0; j < 16; ++j) ld(a1, b1, j, nsub > 1 ? 1 : 0, true);
+    if constexpr (kFlags & (kW4NoA | kW4NoB)) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ld(a2, b2, j, nsub > 2 ? 2 : 0, true);
+    }
     int u = 0;
     for (; u + 3 <= nsub; u += 3) {
         constexpr bool kLd = !(kFlags & kW4NoRead);  // ablation: MFMAs on stale registers, no loads
+        if constexpr (kFlags & kW4Sync) __builtin_amdgcn_s_barrier();  // keep the 4 waves within a step (L1 reuse)
         substep(a0, b0, a2, b2, u + 2, kLd);                  // u + 2 < nsub
         substep(a1, b1, a0, b0, u + 3, kLd);                  // clamped past the end
         substep(a2, b2, a1, b1, u + 4, kLd);

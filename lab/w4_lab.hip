@@ -65,6 +65,12 @@ int main(int argc, char **argv) {
         {"ppF", gemm_i8_pp<2, kEpiNone, kPPLayoutF>, 512, true},
         {"ppF_nostore", gemm_i8_pp<2, kEpiNone, kPPLayoutF | kPPNoStore>, 512, true},
         {"f4_noload_ns", gemm_i8_f4<kW4NoStore | kW4NoRead>, 256, true},
+        {"f4_noA_ns", gemm_i8_f4<kW4NoStore | kW4NoA>, 256, true},
+        {"f4_noB_ns", gemm_i8_f4<kW4NoStore | kW4NoB>, 256, true},
+        {"f4_k1_ns", gemm_i8_f4<kW4NoStore | kW4K1>, 256, true},
+        {"f4sync", gemm_i8_f4<kW4Sync>, 256, true},
+        {"f4sync_nostore", gemm_i8_f4<kW4Sync | kW4NoStore>, 256, true},
+        {"f4_k4_ns", gemm_i8_f4<kW4NoStore | kW4K4>, 256, true},
     };
     dim3 grid(p.tiles_m * p.tiles_n);
     if (only && std::string(only) == "clock") {
@@ -81,9 +87,21 @@ int main(int argc, char **argv) {
             {"w4s_nostore", gemm_i8_w4s<kW4Stamp | kW4NoStore>, 256, w4_sym},
             {"f4", gemm_i8_f4<kW4Stamp>, 256, w4_sym},
             {"f4_nostore", gemm_i8_f4<kW4Stamp | kW4NoStore>, 256, w4_sym},
+            {"f4_noload_ns", gemm_i8_f4<kW4Stamp | kW4NoStore | kW4NoRead>, 256, w4_sym},
+            {"f4_noB_ns", gemm_i8_f4<kW4Stamp | kW4NoStore | kW4NoB>, 256, w4_sym},
+            {"f4_k1_ns", gemm_i8_f4<kW4Stamp | kW4NoStore | kW4K1>, 256, w4_sym},
+            {"f4sync", gemm_i8_f4<kW4Stamp | kW4Sync>, 256, w4_sym},
+            {"f4_k4_ns", gemm_i8_f4<kW4Stamp | kW4NoStore | kW4K4>, 256, w4_sym},
             {"ppF", gemm_i8_pp<2, kEpiNone, kPPStamp | kPPLayoutF>, 512, pp_sym},
         };
         const int nb = p.tiles_m * p.tiles_n;
+        if (argc > 6) {  // clock mode: optional name filter
+            std::vector<SV> keep;
+            const std::string list = std::string(",") + argv[6] + ",";
+            for (auto &v : sv)
+                if (list.find(std::string(",") + v.name + ",") != std::string::npos) keep.push_back(v);
+            sv = keep;
+        }
         for (auto &v : sv) {
             hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
             int launches = 0; float ms = 0;
@@ -108,6 +126,16 @@ int main(int argc, char **argv) {
             auto med = [](std::vector<double> x) { std::sort(x.begin(), x.end()); return x[x.size() / 2]; };
             printf("%-14s avg launch %7.2f us  loop: clock %.3f GHz, %6.2f us/block  epilogue: clock %.3f GHz, %6.2f us/block\n",
                    v.name, ms * 1000 / launches, med(lc), med(lu), med(ec), med(eu));
+            // skew of the LAST launch (realtime stamps, 100 MHz): starts, loop ends, block ends vs the first start
+            unsigned long long s0 = ~0ull, s1 = 0, l0 = ~0ull, l1 = 0, e0 = ~0ull, e1 = 0;
+            for (int i = 0; i < nb; ++i) {
+                const unsigned long long *q = &st[(size_t)i * 6];
+                s0 = std::min(s0, q[1]); s1 = std::max(s1, q[1]);
+                l0 = std::min(l0, q[3]); l1 = std::max(l1, q[3]);
+                e0 = std::min(e0, q[5]); e1 = std::max(e1, q[5]);
+            }
+            printf("%-14s   skew (us from first start): starts %.2f..%.2f  loop ends %.2f..%.2f  block ends %.2f..%.2f\n",
+                   v.name, 0.0, (s1 - s0) * 0.01, (l0 - s0) * 0.01, (l1 - s0) * 0.01, (e0 - s0) * 0.01, (e1 - s0) * 0.01);
         }
         return 0;
     }

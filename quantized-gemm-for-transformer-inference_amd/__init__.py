@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "qgemm_set_gemm_events",
     "qgemm_set_event_mode",
     "qgemm_fill_uniform",
+    "qgemm_gemm_plan",
     "qgemm_version",
 )
 
@@ -169,6 +170,8 @@ def load() -> ctypes.CDLL:
         L.qgemm_set_gemm_events.restype = i32
         L.qgemm_set_event_mode.argtypes = [i32]
         L.qgemm_set_event_mode.restype = i32
+        L.qgemm_gemm_plan.argtypes = [i32, i32, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p)]
+        L.qgemm_gemm_plan.restype = i32
         L.qgemm_version.argtypes = []
         L.qgemm_version.restype = ctypes.c_char_p
         _lib = L

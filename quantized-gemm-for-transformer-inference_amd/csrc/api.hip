@@ -367,6 +367,11 @@ int qgemm_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float
     return err(launch_fill_uniform(dst, count, seed, lo, hi, static_cast<hipStream_t>(stream)));
 }
 
+int qgemm_gemm_plan(int m, int n, int k, int *tile, const char **kernel) {
+    if (m < 1 || n < 1 || k < 1) return -(int)hipErrorInvalidValue;
+    return gemm_plan_info(m, n, round_up(k, kKPad), tile, kernel);
+}
+
 const char *qgemm_version(void) {
     static char buf[160];
     snprintf(buf, sizeof buf, "qgemm 0.1.0 gfx950 %s", gemm_config_name());

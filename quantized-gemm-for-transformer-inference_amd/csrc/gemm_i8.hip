@@ -7,6 +7,8 @@
 // by one kernel that reads the packed int8 operands once per macro-tile and writes fp32 O once.
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
+
 #include "gemm_i8_kernels.h"
 
 namespace qgemm {
@@ -16,6 +18,11 @@ using namespace gemm;
 const char *gemm_config_name() { return "i8mfma16x16x64_t256x256_w4_wt128x128_fragmajor_direct_agpr"; }
 
 static thread_local GemmEvents t_events;
+// split-K 256-tile plans: 0 = gemm_i8_fm (product), 1 = the ping-pong kernel (QGEMM_SPLIT_KERNEL=pp: A/B)
+static const int g_split_kernel = [] {
+    const char *e = getenv("QGEMM_SPLIT_KERNEL");
+    return e && e[0] == 'p' ? 1 : 0;
+}();
 static int g_event_mode = 0;  // 0: hipExtLaunchKernel events, 1: hipEventRecord around the launch
 void set_gemm_event_mode(int mode) { g_event_mode = mode; }
 void set_gemm_events(hipEvent_t start, hipEvent_t stop) { t_events = GemmEvents{start, stop}; }
@@ -76,6 +83,25 @@ static GemmPlan gemm_plan(int m, int n, int k) {
 
 int gemm_splits(int m, int n, int k) { return gemm_plan(m, n, k).splits; }
 
+int gemm_plan_info(int m, int n, int k, int *tile, const char **kernel) {
+    const GemmPlan g = gemm_plan(m, n, k);
+    if (tile) *tile = g.tile;
+    if (kernel) {
+        if (g.tile == 32) *kernel = "gemm_i8_small<32> (32x32 tiles, 4 waves of 16x16, 4-stage LDS-DMA ring)";
+        else if (g.tile == 64)
+            *kernel = g.splits > 1 ? "gemm_i8_small<64> (64x64 tiles, LDS-DMA ring, split-K)"
+                                   : "gemm_i8_small<64> (64x64 tiles, LDS-DMA ring)";
+        else if (g.splits > 1 && (g_split_kernel == 1 || g.splits != 2))
+            *kernel = "gemm_i8_pp<2> (256x256 tiles, 8 waves ping-pong, LDS-DMA ring, split-K)";
+        else
+            *kernel = g.splits > 1 ? "gemm_i8_fm<split-K> (256x256 tiles, 4 waves of 128x128, fragment-major operands "
+                                     "straight to VGPRs, AGPR accumulators, int32 slabs + tickets)"
+                                   : "gemm_i8_fm (256x256 tiles, 4 waves of 128x128, fragment-major operands straight to "
+                                     "VGPRs, AGPR accumulators, fused dequant epilogue)";
+    }
+    return g.splits;
+}
+
 // One fixed ticket region at the start of every split-K scratch (splits happen only below 320 tiles):
 // shapes that share a library-owned scratch then never write slabs over each other's tickets.
 constexpr size_t kTicketBytes = 4096;
@@ -102,8 +128,8 @@ __global__ __launch_bounds__(256) void zero_tickets_kernel(unsigned *__restrict_
 }
 
 // 256 x 256 tiles: gemm_i8_fm (4 waves of 128 x 128, operands straight from the fragment-major packed
-// layout, no LDS in the main loop) where the tile is not split; the ping-pong kernel (gemm_i8_pp<2>, on the
-// same layout) for split-K plans and the LLM.int8() outlier epilogue, which it implements.
+// layout, no LDS in the main loop), split-K plans included; the ping-pong kernel (gemm_i8_pp<2>, on the same
+// layout) for the LLM.int8() outlier epilogue, which it implements.
 template <typename Launch>
 static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const GemmArgs &p, Launch kernel) {
     const GemmEvents ev = take_gemm_events();
@@ -120,9 +146,12 @@ static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const 
 
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
-    if (p.splits > 1 || kEpi == kEpiOutlier)
+    if (kEpi == kEpiOutlier || (p.splits > 1 && (g_split_kernel == 1 || p.splits != 2)))
         return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF>);
-    if constexpr (kEpi != kEpiOutlier) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);
+    if constexpr (kEpi != kEpiOutlier) {
+        if (p.splits > 1) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, true>);
+        return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);
+    }
     return hipErrorNotSupported;
 }
 

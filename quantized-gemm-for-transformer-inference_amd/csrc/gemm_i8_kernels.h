@@ -997,25 +997,63 @@ __device__ __forceinline__ const int8_t *uniform_ptr(const int8_t *q) {
 
 constexpr int kFmThreads = 256;
 
-template <int kEpi = kEpiNone, bool kI32 = false>
+// Split-K arrival for gemm_i8_fm (two K slices per tile, the only split the 256-tile plan makes): the same
+// write-through protocol as splitk_combine -- this slice's AGPR accumulators stored to its slab with sc1
+// stores, drained, then a relaxed agent-scope ticket.  Returns true in the slice that arrives last; its
+// epilogue adds the other slab's partial sums (sc1 loads, after the ticket) as it reads the accumulators, so
+// no accumulator is copied out of the AGPRs.
+__device__ __forceinline__ bool splitk_arrive_fm(const GemmArgs &p, unsigned *last, v4i (&acc)[8][8], int tile,
+                                                 int slice, int wave, int lane, int tid) {
+    constexpr int S = 2;
+    constexpr int kSlabBytes = 4 * 8 * 8 * 64 * 16;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char *>(p.slabs) + (int64_t)tile * S * kSlabBytes, 0, S * kSlabBytes, 0x00020000);
+    const int lane_off = (wave * 64 * 64 + lane) * 16;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni)
+            __builtin_amdgcn_raw_buffer_store_b128(acc[mi][ni], rsrc, slice * kSlabBytes + lane_off + (mi * 8 + ni) * 1024,
+                                                   0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned t = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last = t;
+        if (t == (unsigned)(S - 1) && p.reset_tickets)
+            __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return *last == (unsigned)(S - 1);
+}
+
+template <int kEpi = kEpiNone, bool kI32 = false, bool kSplit = false>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
+    static_assert(!(kI32 && kSplit), "raw accumulators are not split");
     constexpr int TS = 132;                 // padded row of a wave's epilogue block (conflict-free ds_write)
     constexpr int kBlockBytes = 64 * TS * 4;
-    __shared__ __attribute__((aligned(16))) int8_t lds[4 * kBlockBytes + 2048];
+    __shared__ __attribute__((aligned(16))) int8_t lds[4 * kBlockBytes + 2048 + 16];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
+    // XCD remap first, then tile = id / S, slice = id % S (split-K: a tile's slices share an XCD)
+    const int S = kSplit ? 2 : 1;  // the 256-tile plan splits in two or not at all (host checks)
+    const int wid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = wid / S, slice = wid - tile * S;
     int tm, tn;
-    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
     const int nsub = (int)(p.k_pad / 64);
-    // this wave's half panels: 8 row groups x nsub blocks each (= 128 packed rows)
-    const int half_bytes = 8 * nsub * 1024;
+    // this slice's sub-steps [u0, u0 + nloc) of the nsub 64-deep k-blocks
+    const int u0 = __builtin_amdgcn_readfirstlane(slice * nsub / S);
+    const int nloc = __builtin_amdgcn_readfirstlane((slice + 1) * nsub / S - u0);
+    // this wave's half panels: 8 row groups x nsub blocks each (= 128 packed rows), from block u0 on
+    const int half_bytes = 8 * nsub * 1024 - u0 * 1024;
     const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int8_t *>(uniform_ptr(p.A + ((int64_t)tm * 16 + wm * 8) * nsub * 1024)), 0,
+        const_cast<int8_t *>(uniform_ptr(p.A + (((int64_t)tm * 16 + wm * 8) * nsub + u0) * 1024)), 0,
         __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
     const auto rsB = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int8_t *>(uniform_ptr(p.B + ((int64_t)tn * 16 + wn * 8) * nsub * 1024)), 0,
+        const_cast<int8_t *>(uniform_ptr(p.B + (((int64_t)tn * 16 + wn * 8) * nsub + u0) * 1024)), 0,
         __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
     const int voff = lane * 16;
 
@@ -1036,7 +1074,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     // across the loop and spill a register set)
     auto substep = [&](v4i (&ca)[8], v4i (&cb)[8], v4i (&na)[8], v4i (&nb)[8], int un, bool more)
                        __attribute__((always_inline)) {
-        un = un < nsub ? un : nsub - 1;
+        un = un < nloc ? un : nloc - 1;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi) {
@@ -1053,20 +1091,29 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) ld(a0, b0, j, 0);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ld(a1, b1, j, nsub > 1 ? 1 : 0);
+    for (int j = 0; j < 16; ++j) ld(a1, b1, j, nloc > 1 ? 1 : 0);
     int u = 0;
-    for (; u + 3 <= nsub; u += 3) {
+    for (; u + 3 <= nloc; u += 3) {
         substep(a0, b0, a2, b2, u + 2, true);
         substep(a1, b1, a0, b0, u + 3, true);
         substep(a2, b2, a1, b1, u + 4, true);
     }
-    const int rest = nsub - u;  // 0, 1 or 2: sets 0 and 1 hold sub-steps u, u+1
+    const int rest = nloc - u;  // 0, 1 or 2: sets 0 and 1 hold sub-steps u, u+1
     if (rest > 0) {
         substep(a0, b0, a2, b2, 0, false);
         if (rest > 1) substep(a1, b1, a2, b2, 0, false);
     }
     // the last MFMAs' results are read by VALU below; the asm statements hide them from hipcc's padding
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    if constexpr (kSplit) {
+        {
+            // split-K: slabs + arrival ticket (write-through form, see splitk_combine); the last slice of
+            // the tile holds the complete sums and runs the epilogue
+            unsigned *last = reinterpret_cast<unsigned *>(lds + 4 * kBlockBytes + 2048);
+            if (!splitk_arrive_fm(p, last, acc, tile, slice, wave, lane, tid)) return;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: slab loads stay below
+        }
+    }
 
     const int gi0 = tm * BM, gj0 = tn * BN;
     const int lrow = lane & 15, kq = lane >> 4;
@@ -1092,6 +1139,21 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+        // split-K reducer: the other slice's partial sums of this half (32 sc1 loads in flight, then the adds)
+        v4i oth[4][8];
+        if constexpr (kSplit) {
+            constexpr int kSlabBytes = 4 * 8 * 8 * 64 * 16;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<char *>(p.slabs) + ((int64_t)tile * 2 + (1 - slice)) * kSlabBytes, 0, kSlabBytes,
+                0x00020000);
+            const int lane_off = (wave * 64 * 64 + lane) * 16;
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni)
+                    oth[mq][ni] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + ((4 * s + mq) * 8 + ni) * 1024,
+                                                                        0, 16 /* sc1 */);
+        }
         float cxv[4][4];
 #pragma unroll
         for (int mq = 0; mq < 4; ++mq)
@@ -1109,7 +1171,8 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
                     if constexpr (kI32) {
                         o = __int_as_float(acc[4 * s + mq][ni][r]);  // the raw bits travel through LDS
                     } else {
-                        o = dequantize(acc[4 * s + mq][ni][r], outer_product(cxv[mq][r], cwv[ni]), p.inv_r2);
+                        const int a = kSplit ? acc[4 * s + mq][ni][r] + oth[mq][ni][r] : acc[4 * s + mq][ni][r];
+                        o = dequantize(a, outer_product(cxv[mq][r], cwv[ni]), p.inv_r2);
                         if constexpr (has_bias(kEpi)) o = __fadd_rn(o, bv[ni]);
                         if constexpr (kEpi == kEpiBiasRelu) o = (o < 0.0f) ? 0.0f : o;
                     }

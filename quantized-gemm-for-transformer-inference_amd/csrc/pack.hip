@@ -17,6 +17,8 @@
 //               (op_reduction.cuh:96-117) + 2 elementwise launches.
 //   pack_rows_and_colmax : pack_rows(A) and pass 1 of pack_cols(B) in ONE launch (block roles), so
 //               the two HBM streams overlap and a launch boundary disappears.
+#include <algorithm>
+
 #include "qgemm_internal.h"
 
 namespace qgemm {
@@ -47,6 +49,23 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+// W strips hold 4 consecutive k of one column per dword; a 16-B piece of the fragment-major q (one packed row,
+// 16 consecutive k) is the dwords d[col] of the 4 threads b = 0..3 of a quad (lanes qbase + stride * b) that
+// hold k = 16a + 4b.  4 x 4 transpose among them: returns, in thread b, the piece of the quad's column b.
+// Round rr: send d[(b - rr) & 3], receive from quad thread (b + rr) & 3 its d[b] = piece dword (b + rr) & 3.
+__device__ __forceinline__ void quad_transpose(const uint32_t (&d)[4], int b, int qbase, int stride,
+                                               uint32_t (&pc)[4]) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        const int si = (b - rr) & 3;
+        const uint32_t x = si == 0 ? d[0] : si == 1 ? d[1] : si == 2 ? d[2] : d[3];
+        const int from = (b + rr) & 3;
+        const uint32_t y = (uint32_t)__shfl((int)x, qbase + stride * from, 64);
+#pragma unroll
+        for (int sl = 0; sl < 4; ++sl) pc[sl] = from == sl ? y : pc[sl];
+    }
+}
+
 // wave-uniform buffer descriptor over [base, base + bytes): loads past the end return zeros
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
@@ -64,6 +83,22 @@ template <bool kWT>
 __device__ __forceinline__ void st_f32(float *p, float v) {
     if constexpr (kWT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
+}
+
+// Blocks b and b + 8 run on one XCD.  For a role occupying blocks [base, base + count): a role-local index
+// that gives every XCD ONE contiguous range (bijective).  Row packs index their rows with it: a 128-B line
+// of the fragment-major q holds 16-B pieces of 8 consecutive rows (qgemm_internal.h fofs), and rows packed
+// on 8 different XCDs would leave every line as 8 partial writes from 8 L2s (FFN-down X rows, one row per
+// block: 116 vs 89 us before this mapping).
+__device__ __forceinline__ int xcd_contig(int bid, int base, int count) {
+    const int x = bid & 7;
+    int start = 0;
+#pragma unroll
+    for (int y = 0; y < 7; ++y) {
+        const int o = (y - base) & 7;
+        if (y < x && o < count) start += (count - 1 - o) / 8 + 1;
+    }
+    return start + (bid - base - ((x - base) & 7)) / 8;
 }
 
 // The GEMM's split-K tickets live in the caller's workspace, whose contents are arbitrary: the pack
@@ -94,20 +129,25 @@ __device__ __forceinline__ bool om_bit(const OutlierMask &om, int k) { return (o
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
 // R > 0: each lane keeps R float4 chunks in registers (len <= 256*R), one HBM read.
 // R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
-template <int R, bool kMask = false, bool kWT = false>
+// kStage: the packed row goes to `stage` (the wave's LDS row, dword c at stage[c]) instead of q; the caller
+// writes the block's staged rows out as whole 128-B lines of the fragment-major q (write_staged_rows).
+template <int R, bool kMask = false, bool kWT = false, bool kStage = false>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
-                                                   const OutlierMask *om = nullptr) {
+                                                   const OutlierMask *om = nullptr, uint32_t *stage = nullptr) {
     static_assert(!kMask || R > 0, "the outlier mask needs the register-resident rows");
     const int lane = threadIdx.x & 63;
     const int64_t row = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     if (row >= rows_pad) return;
-    // dword c of the packed row (k = 4c), fragment-major layout (qgemm_internal.h fofs)
-    auto qrow = [&](int64_t c) __attribute__((always_inline)) { return qword(q, row, 4 * c, k_pad); };
+    // dword c of the packed row (k = 4c), fragment-major layout (qgemm_internal.h fofs), or of the LDS stage
+    auto put = [&](int64_t c, uint32_t v) __attribute__((always_inline)) {
+        if constexpr (kStage) stage[c] = v;
+        else st_u32<kWT>(qword(q, row, 4 * c, k_pad), v);
+    };
     const int64_t nq = k_pad >> 2;  // uint32 words per packed row
     if (row >= rows) {              // padding row
-        for (int64_t c = lane; c < nq; c += kWave) st_u32<kWT>(qrow(c), 0u);
+        for (int64_t c = lane; c < nq; c += kWave) put(c, 0u);
         if (lane == 0) st_f32<kWT>(scale + row, 0.0f);
         return;
     }
@@ -202,13 +242,12 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         for (int j = 0; j < R; ++j) {
             const int c = lane + j * kWave;
             if (c < nfull)
-                st_u32<kWT>(qrow(c), pack4(quant_i8(v[j].x, s), quant_i8(v[j].y, s), quant_i8(v[j].z, s),
-                                            quant_i8(v[j].w, s)));
+                put(c, pack4(quant_i8(v[j].x, s), quant_i8(v[j].y, s), quant_i8(v[j].z, s), quant_i8(v[j].w, s)));
         }
     } else {
         for (int c = lane; c < nfull; c += kWave) {
             float4 x = s4[c];
-            st_u32<kWT>(qrow(c), pack4(quant_i8(x.x, s), quant_i8(x.y, s), quant_i8(x.z, s), quant_i8(x.w, s)));
+            put(c, pack4(quant_i8(x.x, s), quant_i8(x.y, s), quant_i8(x.z, s), quant_i8(x.w, s)));
         }
     }
     // partial tail word, then zero padding words
@@ -216,10 +255,29 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
     if ((len & 3) && lane == 0) {
         int b[4] = {0, 0, 0, 0};
         for (int e = 0; e < (len & 3); ++e) b[e] = quant_i8(srow[tail0 + e], s);
-        st_u32<kWT>(qrow(nfull), pack4(b[0], b[1], b[2], b[3]));
+        put(nfull, pack4(b[0], b[1], b[2], b[3]));
     }
-    for (int64_t c = first_zero + lane; c < nq; c += kWave) st_u32<kWT>(qrow(c), 0u);
+    for (int64_t c = first_zero + lane; c < nq; c += kWave) put(c, 0u);
     if (lane == 0) st_f32<kWT>(scale + row, cx);
+}
+
+// Staged packed rows: kRows (8 or 16) consecutive packed rows row0 .. (row0 % 8 == 0), one per wave, in LDS
+// at stage + r * rsw dwords (rsw = k_pad / 4 + 8: rows 8 banks apart, so the 16-B reads below are
+// conflict-free), written out as whole 128-B lines of the fragment-major q: line (L, h) = the 16-B pieces
+// of k 16L .. 16L+15 of rows 8h .. 8h+7; one wave store instruction = 8 lines.  After a block barrier.
+constexpr int kStageRowWordsMax = 4096 / 4 + 8;
+template <int kRows>
+__device__ __forceinline__ void write_staged_rows(const uint32_t *stage, int rsw, int8_t *__restrict__ q, int64_t row0,
+                                                  int64_t k_pad) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int nl = (int)(k_pad >> 4);  // 16-B pieces per row (a multiple of 8)
+    const int units = nl * (kRows / 8);
+    for (int u = wv * 8 + (lane >> 3); u < units; u += kRows * 8) {
+        const int h = u / nl, L = u - h * nl;
+        const int r = h * 8 + (lane & 7);
+        const uint4 v = *reinterpret_cast<const uint4 *>(stage + r * rsw + 4 * L);
+        *reinterpret_cast<uint4 *>(q + fofs(row0 + r, 16 * L, k_pad)) = v;
+    }
 }
 
 // pack_rows, long rows (4096 < len <= 16384): ONE 256-thread block per row, up to 16 float4 per
@@ -289,7 +347,7 @@ __global__ __launch_bounds__(256) void pack_rows_block_kernel(const float *__res
                                                               int8_t *__restrict__ q, int64_t rows_pad,
                                                               int64_t k_pad) {
     __shared__ float red[8];
-    pack_row_block_body(blockIdx.x, src, sh, rows, len, range, scale, q, rows_pad, k_pad, red);
+    pack_row_block_body(xcd_contig(blockIdx.x, 0, gridDim.x), src, sh, rows, len, range, scale, q, rows_pad, k_pad, red);
 }
 
 template <int R>
@@ -297,7 +355,7 @@ __global__ __launch_bounds__(256) void pack_rows_vec_kernel(const float *__restr
                                                             int len, float range, float *__restrict__ scale,
                                                             int8_t *__restrict__ q, int64_t rows_pad,
                                                             int64_t k_pad) {
-    pack_rows_vec_body<R>(blockIdx.x, src, sh, rows, len, range, scale, q, rows_pad, k_pad);
+    pack_rows_vec_body<R>(xcd_contig(blockIdx.x, 0, gridDim.x), src, sh, rows, len, range, scale, q, rows_pad, k_pad);
 }
 
 // pack_rows, generic strides (any sh, sw): scalar loads, two passes.
@@ -306,7 +364,7 @@ __global__ __launch_bounds__(256) void pack_rows_generic_kernel(const float *__r
                                                                 float *__restrict__ scale, int8_t *__restrict__ q,
                                                                 int64_t rows_pad, int64_t k_pad) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)xcd_contig(blockIdx.x, 0, gridDim.x) * 4 + (threadIdx.x >> 6);
     if (row >= rows_pad) return;
     auto qrow = [&](int64_t c) __attribute__((always_inline)) -> int8_t & { return q[fofs(row, c, k_pad)]; };
     if (row >= rows) {
@@ -399,9 +457,11 @@ __global__ __launch_bounds__(256) void pack_rows_and_colmax_kernel(
         // unrolled 4 deep: pack3_lab `call_u4` 140.9-146.0 vs 143.6-149.4 us for 8 (FFN down, pass 1 + pass 2)
         colmax_body<true, 4>(bid % col_blocks, bid / col_blocks, b, bsh, k, n, b_partial, b_rows_pad, red);
     } else if constexpr (R < 0) {
-        pack_row_block_body(bid - ncol, a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad, red);
+        pack_row_block_body(xcd_contig(bid, ncol, gridDim.x - ncol), a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad,
+                            red);
     } else {
-        pack_rows_vec_body<R>(bid - ncol, a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad);
+        pack_rows_vec_body<R>(xcd_contig(bid, ncol, gridDim.x - ncol), a, ash, m, k, range, a_scale, a_q, a_rows_pad,
+                              k_pad);
     }
 }
 
@@ -577,25 +637,36 @@ __device__ __forceinline__ void pack_w_strip_body(int strip, const float *__rest
     }
     __syncthreads();
     const float s0 = s_sh[4 * c4 + 0], s1 = s_sh[4 * c4 + 1], s2 = s_sh[4 * c4 + 2], s3 = s_sh[4 * c4 + 3];
-    // quantize; 4 consecutive rows of one column = one dword of packed row n0+4c4+cc, stored directly:
-    // per wave instruction 4 runs of 64 B (16 rq lanes), the neighbouring waves complete each line in
-    // L2 (an LDS transpose to whole-row 16-B stores measured ~1 us slower per launch)
+    // quantize; 4 consecutive rows of one column = one dword of packed row n0 + 4 c4 + cc.  The quad of threads
+    // rq = 4a .. 4a+3 with the same c4 (lanes 4 rq + c4) hold the 16 k of a fragment-major piece: after the quad
+    // transpose thread b = rq & 3 stores the piece of packed row n0 + 4 c4 + b, and one wave store instruction
+    // writes a whole 1-KiB block (16 rows x 64 k).
+    const auto dst = buf_rsrc(q + n0 * k_pad, (uint32_t)(16 * k_pad));
+    const int b = rq & 3;
+    const int qbase = lane - 4 * b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r0 = 4 * rq + 1024 * i;
-        if (r0 >= k_pad) continue;
-        int qv[4][4];  // [e][col]
+        uint32_t d[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const bool in = r0 + e < k;
-            qv[e][0] = in ? quant_i8(v[i][e].x, s0) : 0;
-            qv[e][1] = in ? quant_i8(v[i][e].y, s1) : 0;
-            qv[e][2] = in ? quant_i8(v[i][e].z, s2) : 0;
-            qv[e][3] = in ? quant_i8(v[i][e].w, s3) : 0;
+        for (int cc = 0; cc < 4; ++cc) {
+            int qe[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = cc == 0 ? v[i][e].x : cc == 1 ? v[i][e].y : cc == 2 ? v[i][e].z : v[i][e].w;
+                const float sc = cc == 0 ? s0 : cc == 1 ? s1 : cc == 2 ? s2 : s3;
+                qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
+            }
+            d[cc] = pack4(qe[0], qe[1], qe[2], qe[3]);
         }
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc)
-            *qword(q, n0 + 4 * c4 + cc, r0, k_pad) = pack4(qv[0][cc], qv[1][cc], qv[2][cc], qv[3][cc]);
+        uint32_t pc[4] = {0u, 0u, 0u, 0u};
+        quad_transpose(d, b, qbase, 4, pc);
+        const int kp = r0 - 4 * b;
+        if (kp < k_pad) {
+            typedef int v4i_t __attribute__((ext_vector_type(4)));
+            const v4i_t val = {(int)pc[0], (int)pc[1], (int)pc[2], (int)pc[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(val, dst, (uint32_t)fofs(4 * c4 + b, kp, k_pad), 0, 0);
+        }
     }
 }
 
@@ -620,9 +691,15 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
         zero_packed_rows(w_q, n0, kWsCols, k_pad, threadIdx.x, 1024);
         if (threadIdx.x < kWsCols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
-        // X rows: 16 rows per 1024-thread block = four 4-row groups of the 256-thread body
+        // X rows: 16 rows per 1024-thread block = four 4-row groups of the 256-thread body (rows 16xb + (t>>6)),
+        // staged in LDS and written out as whole 1-KiB blocks of the fragment-major q
         const int64_t xb = bid - nstrips - (int)((w_rows_pad - n) / kWsCols);
-        pack_rows_vec_body<16>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad);  // rows 16xb + (t>>6)
+        const int rsw = (int)(k_pad >> 2) + 8;
+        uint32_t *xstage = reinterpret_cast<uint32_t *>(dyn_lds);
+        pack_rows_vec_body<16, false, false, true>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, nullptr,
+                                                   xstage + (threadIdx.x >> 6) * rsw);
+        __syncthreads();
+        write_staged_rows<16>(xstage, rsw, x_q, xb * 16, k_pad);
     }
 }
 
@@ -725,6 +802,7 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
     __syncthreads();
     const float s0 = s_sh[4 * c8 + 0], s1 = s_sh[4 * c8 + 1], s2 = s_sh[4 * c8 + 2], s3 = s_sh[4 * c8 + 3];
     // the strip's 32 packed rows = two whole 16-row groups: one contiguous region of the fragment-major q
+    // (dword stores: the quad transpose to 16-B pieces spilled here, 128 VGPRs, and measured slower)
     const auto dst = buf_rsrc(q + n0 * k_pad, (uint32_t)(kW32Cols * k_pad));
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -766,8 +844,14 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
         zero_packed_rows(w_q, n0, kW32Cols, k_pad, threadIdx.x, 1024);
         if (threadIdx.x < kW32Cols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
+        // 16 rows per block, staged in LDS (the strip role's DMA region) and written out as whole 1-KiB blocks
         const int64_t xb = bid - nstrips - npad;
-        pack_rows_vec_body<16>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad);
+        const int rsw = (int)(k_pad >> 2) + 8;
+        uint32_t *xstage = reinterpret_cast<uint32_t *>(lds_w);
+        pack_rows_vec_body<16, false, false, true>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, nullptr,
+                                                   xstage + (threadIdx.x >> 6) * rsw);
+        __syncthreads();
+        write_staged_rows<16>(xstage, rsw, x_q, xb * 16, k_pad);
     }
 }
 
@@ -877,15 +961,21 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     }
     __syncthreads();
     const float s0 = s_sh[4 * c2 + 0], s1 = s_sh[4 * c2 + 1], s2 = s_sh[4 * c2 + 2], s3 = s_sh[4 * c2 + 3];
-    // 4 consecutive rows of one column = one dword of packed row n0 + 4*c2 + cc
-    // the strip's 8 packed rows are half of a 16-row group of the fragment-major q: descriptor over the group
+    // 4 consecutive rows of one column = one dword of packed row n0 + 4*c2 + cc.  The strip's 8 packed rows are
+    // half of a 16-row group of the fragment-major q (descriptor over the group), and a 16-B piece of it (one
+    // packed row, 16 consecutive k) is the dwords of the 4 threads rq = 4a .. 4a+3 with the same c2 (lanes
+    // 2 rq + c2).  A 4 x 4 transpose among those lanes (4 shuffles) leaves thread b = rq & 3 holding the piece of
+    // packed row 4 c2 + b, so one wave store instruction writes 16 B per lane = 8 whole 128-B lines (rows 0-7
+    // of the group, 2 k-blocks x 4 k-chunks), not 4-B pieces of 16 lines.
     const int64_t g0 = n0 & ~(int64_t)15;
     const auto dst = buf_rsrc(q + g0 * k_pad, (uint32_t)(16 * k_pad));
-    const int rr0 = (int)(n0 - g0) + 4 * c2;
+    const int b = rq & 3;
+    const int qbase = lane - 2 * b;  // lane of this quad's b = 0 thread
+    const int prow = (int)(n0 - g0) + 4 * c2 + b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r0 = 4 * rq + 1024 * i;
-        if (r0 >= k_pad) continue;
+        uint32_t d[4];
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
             int qe[4];
@@ -895,8 +985,15 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
                 const float sc = cc == 0 ? s0 : cc == 1 ? s1 : cc == 2 ? s2 : s3;
                 qe[e] = (r0 + e < k) ? quant_i8(x, sc) : 0;
             }
-            __builtin_amdgcn_raw_buffer_store_b32((int)pack4(qe[0], qe[1], qe[2], qe[3]), dst,
-                                                  (uint32_t)fofs(rr0 + cc, r0, k_pad), 0, kWT ? 16 /* sc1 */ : 0);
+            d[cc] = pack4(qe[0], qe[1], qe[2], qe[3]);
+        }
+        uint32_t pc[4] = {0u, 0u, 0u, 0u};
+        quad_transpose(d, b, qbase, 2, pc);
+        const int kp = r0 - 4 * b;  // the piece's first k (a multiple of 16)
+        if (kp < k_pad) {
+            typedef int v4i_t __attribute__((ext_vector_type(4)));
+            const v4i_t val = {(int)pc[0], (int)pc[1], (int)pc[2], (int)pc[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(val, dst, (uint32_t)fofs(prow, kp, k_pad), 0, kWT ? 16 /* sc1 */ : 0);
         }
     }
 }
@@ -908,6 +1005,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
     int8_t *__restrict__ w_q, int64_t w_rows_pad, int nstrips, float range, uint32_t *zero_words, int nzero,
     OutlierMask om = OutlierMask{}) {
     __shared__ float red[8 * 8 + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t xstage[8 * kStageRowWordsMax];  // X rows, LDS-staged
     const int bid = blockIdx.x;
     zero_words_block0(zero_words, nzero);
     const int npad = (int)((w_rows_pad - n) / kWs8Cols);
@@ -921,8 +1019,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         zero_packed_rows(w_q, n0, kWs8Cols, k_pad, threadIdx.x, 512);
         if (threadIdx.x < kWs8Cols) w_scale[n0 + threadIdx.x] = 0.0f;
     } else {
-        const int64_t xb = bid - nstrips - npad;  // rows 8xb + (t>>6): two 4-row groups of the 256-thread body
-        pack_rows_vec_body<16, kMask>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om);
+        // rows 8xb + (t>>6): two 4-row groups of the 256-thread body, staged in LDS and written out as whole
+        // 128-B lines of the fragment-major q (a line = 8 rows x 16 B: exactly this block's rows)
+        const int64_t xb = bid - nstrips - npad;
+        const int rsw = (int)(k_pad >> 2) + 8;
+        pack_rows_vec_body<16, kMask, false, true>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om,
+                                                   xstage + (threadIdx.x >> 6) * rsw);
+        __syncthreads();
+        write_staged_rows<8>(xstage, rsw, x_q, xb * 8, k_pad);
     }
 }
 
@@ -1042,7 +1146,12 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
     const int nstrips = n / kWsCols;
     const int npad = (int)((outw.rows_pad - n) / kWsCols);
     const int nx = (int)(outx.rows_pad / 16);
-    const size_t lds = 4096;  // [16 waves][16 cols] partial maxima + 16 scales
+    // W strips: [16 waves][16 cols] partial maxima + 16 scales; X rows: 16 staged packed rows
+    const size_t lds = std::max<size_t>(4096, (size_t)16 * 4 * (outx.k_pad / 4 + 8));
+    static const hipError_t lds_attr = hipFuncSetAttribute(reinterpret_cast<const void *>(pack_single_pass_kernel),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           16 * 4 * kStageRowWordsMax);
+    if (lds_attr != hipSuccess) return lds_attr;
     pack_single_pass_kernel<<<nstrips + npad + nx, 1024, lds, stream>>>(x, xsh, m, k, outx.scale, outx.q, outx.rows_pad,
                                                                          outx.k_pad, w, wsh, n, outw.scale, outw.q,
                                                                          outw.rows_pad, nstrips, range, zero_words,

@@ -141,6 +141,8 @@ hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float l
 // Split-K for shapes with too few 256x256 tiles to fill the chip: gemm_splits() slices per tile and
 // the scratch (tickets + int32 slabs) they need; 1 / 0 when the shape is not split.
 int gemm_splits(int m, int n, int k);
+// the plan's tile edge and kernel name (qgemm_gemm_plan); returns the splits
+int gemm_plan_info(int m, int n, int k, int *tile, const char **kernel);
 size_t gemm_scratch_bytes(int m, int n, int k);
 // scratch: gemm_scratch_bytes(m, n, k) bytes, or nullptr (then no split: correct, slower)
 // bias (n floats) != nullptr: y = fl(O + b[j]) (+ relu): the encoder's linear layers.

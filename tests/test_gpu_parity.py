@@ -191,6 +191,32 @@ def test_split_k_shapes_share_library_scratch(qg, oracle, device):
         assert_bits_equal(O.cpu().numpy(), want, f"call {i}: {M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 4096, 2048), (1900, 4000, 3000), (1800, 4096, 4500)])
+def test_256_tile_split_k_plans(qg, oracle, device, M, N, K):
+    """128 tiles of 256 x 256 with K >= 2048: the split-K plan (S = 2) on gemm_i8_fm -- slabs stored
+    write-through from the AGPR accumulators, the last slice of each tile adds the other slab and runs the
+    epilogue.  Ragged M / N / K edges, K > 4096 (two-pass pack); library scratch twice, then a caller
+    workspace full of 0xFF (tickets zeroed by the pack launch)."""
+    L = qg.load()
+    assert L.qgemm_gemm_plan(M, N, K, None, None) == 2, "shape expected to run the 256-tile split-K plan"
+    X, W = oracle.inputs(M, N, K, 131)
+    X[::7, 0] = -1.5
+    want = oracle.quantized_mm(X, W)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    pa, pb = qg.pack_a(Xd), qg.pack_b(Wd)
+    for i in range(2):
+        O = torch.full((M, N), float("nan"), device=device)
+        qg.mm_packed(pa, pb, O)
+        torch.cuda.synchronize()
+        assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} mm_packed call {i}")
+    ws = torch.full((L.op_mm_quantize_workspace_size(M, N, K),), 255, dtype=torch.uint8, device=device)
+    O = torch.full((M, N), float("nan"), device=device)
+    assert L.op_mm_quantize_ws(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, 127.0,
+                               ws.data_ptr(), ws.numel(), qg._stream(device)) == 0
+    torch.cuda.synchronize()
+    assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} caller workspace")
+
+
 def test_device_generator_matches_oracle(qg, oracle, device):
     t = torch.empty(1 << 20, device=device)
     qg.fill_uniform(t, seed=9)
