@@ -1037,7 +1037,9 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
-    // XCD remap first, then tile = id / S, slice = id % S (split-K: a tile's slices share an XCD)
+    // XCD remap first, then tile = id / S, slice = id % S (split-K: a tile's slices share an XCD).  Measured
+    // alternative (FFN down, kernel trace): XCD pairs taking one 4 x 8 patch of tiles for K half 0 / 1 cut the
+    // operand fetch 404.7 -> 337.6 MB but ran 127.3 us vs 122-126 (the slab then crosses XCDs)
     const int S = kSplit ? 2 : 1;  // the 256-tile plan splits in two or not at all (host checks)
     const int wid = xcd_remap(blockIdx.x, gridDim.x);
     const int tile = wid / S, slice = wid - tile * S;

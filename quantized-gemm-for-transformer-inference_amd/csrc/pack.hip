@@ -262,10 +262,10 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
 }
 
 // Staged packed rows: kRows (8 or 16) consecutive packed rows row0 .. (row0 % 8 == 0), one per wave, in LDS
-// at stage + r * rsw dwords (rsw = k_pad / 4 + 8: rows 8 banks apart, so the 16-B reads below are
-// conflict-free), written out as whole 128-B lines of the fragment-major q: line (L, h) = the 16-B pieces
+// at stage + r * rsw dwords (rsw = k_pad / 4 + 16: the 16-B reads below are conflict-free in ds_read_b128's
+// lane groups for k_pad / 4 = 0 or 32 mod 64; + 8 left 2-way conflicts, 6.5 % of the pack's LDS cycles), written out as whole 128-B lines of the fragment-major q: line (L, h) = the 16-B pieces
 // of k 16L .. 16L+15 of rows 8h .. 8h+7; one wave store instruction = 8 lines.  After a block barrier.
-constexpr int kStageRowWordsMax = 4096 / 4 + 8;
+constexpr int kStageRowWordsMax = 4096 / 4 + 16;
 template <int kRows>
 __device__ __forceinline__ void write_staged_rows(const uint32_t *stage, int rsw, int8_t *__restrict__ q, int64_t row0,
                                                   int64_t k_pad) {
@@ -551,15 +551,22 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
                 qv[i][2] = (kk < len && c + 2 < cols) ? quant_i8(x[h][i].z, s2) : 0;
                 qv[i][3] = (kk < len && c + 3 < cols) ? quant_i8(x[h][i].w, s3) : 0;
             }
+            // packed rows >= 32 (col4 >= 8) have their dwords XOR-swizzled by 2: with the 33-dword stride rows
+            // 4 col4 and 4 (col4 + 8) otherwise share a bank in ds_write_b32's 32-bank lane groups (2-way; r02
+            // PMC 33 % bank-conflict cycles); the read below undoes it (a bijection inside every 8-dword run)
+            const int swz = (col4 >> 3) * 8;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                *reinterpret_cast<uint32_t *>(tb + (4 * col4 + e) * kTStride + 4 * rg + 64 * h) =
+                *reinterpret_cast<uint32_t *>(tb + (4 * col4 + e) * kTStride + ((4 * rg + 64 * h) ^ swz)) =
                     pack4(qv[0][e], qv[1][e], qv[2][e], qv[3][e]);
         }
         __syncthreads();  // tile tb complete (and, double-buffered, the other one is free to rewrite next)
         const uint32_t *lp = reinterpret_cast<const uint32_t *>(tb + n * kTStride + kc);  // 4-B aligned only
-        *reinterpret_cast<uint4 *>(q + fofs(n0 + n, k0 + kc, k_pad)) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
-        *reinterpret_cast<uint4 *>(q + fofs(n0 + n, k0 + kc + 16, k_pad)) = make_uint4(lp[4], lp[5], lp[6], lp[7]);
+        const int rs = (n >> 5) * 2;  // the write's dword swizzle of rows >= 32
+        *reinterpret_cast<uint4 *>(q + fofs(n0 + n, k0 + kc, k_pad)) =
+            make_uint4(lp[0 ^ rs], lp[1 ^ rs], lp[2 ^ rs], lp[3 ^ rs]);
+        *reinterpret_cast<uint4 *>(q + fofs(n0 + n, k0 + kc + 16, k_pad)) =
+            make_uint4(lp[4 ^ rs], lp[5 ^ rs], lp[6 ^ rs], lp[7 ^ rs]);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -694,7 +701,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass_kernel(
         // X rows: 16 rows per 1024-thread block = four 4-row groups of the 256-thread body (rows 16xb + (t>>6)),
         // staged in LDS and written out as whole 1-KiB blocks of the fragment-major q
         const int64_t xb = bid - nstrips - (int)((w_rows_pad - n) / kWsCols);
-        const int rsw = (int)(k_pad >> 2) + 8;
+        const int rsw = (int)(k_pad >> 2) + 16;
         uint32_t *xstage = reinterpret_cast<uint32_t *>(dyn_lds);
         pack_rows_vec_body<16, false, false, true>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, nullptr,
                                                    xstage + (threadIdx.x >> 6) * rsw);
@@ -846,7 +853,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
     } else {
         // 16 rows per block, staged in LDS (the strip role's DMA region) and written out as whole 1-KiB blocks
         const int64_t xb = bid - nstrips - npad;
-        const int rsw = (int)(k_pad >> 2) + 8;
+        const int rsw = (int)(k_pad >> 2) + 16;
         uint32_t *xstage = reinterpret_cast<uint32_t *>(lds_w);
         pack_rows_vec_body<16, false, false, true>(xb * 4, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, nullptr,
                                                    xstage + (threadIdx.x >> 6) * rsw);
@@ -1022,7 +1029,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         // rows 8xb + (t>>6): two 4-row groups of the 256-thread body, staged in LDS and written out as whole
         // 128-B lines of the fragment-major q (a line = 8 rows x 16 B: exactly this block's rows)
         const int64_t xb = bid - nstrips - npad;
-        const int rsw = (int)(k_pad >> 2) + 8;
+        const int rsw = (int)(k_pad >> 2) + 16;
         pack_rows_vec_body<16, kMask, false, true>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om,
                                                    xstage + (threadIdx.x >> 6) * rsw);
         __syncthreads();
@@ -1147,7 +1154,7 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
     const int npad = (int)((outw.rows_pad - n) / kWsCols);
     const int nx = (int)(outx.rows_pad / 16);
     // W strips: [16 waves][16 cols] partial maxima + 16 scales; X rows: 16 staged packed rows
-    const size_t lds = std::max<size_t>(4096, (size_t)16 * 4 * (outx.k_pad / 4 + 8));
+    const size_t lds = std::max<size_t>(4096, (size_t)16 * 4 * (outx.k_pad / 4 + 16));
     static const hipError_t lds_attr = hipFuncSetAttribute(reinterpret_cast<const void *>(pack_single_pass_kernel),
                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                                            16 * 4 * kStageRowWordsMax);

@@ -32,7 +32,8 @@ for s in ${STEPS:-bench prof}; do
     pmc)
       for c in $CFGS; do
         CFG=$c step pmc_$c 600 bash scripts/pmc_bench.sh
-        python3 scripts/summarize_pmc.py gpurun_out/pmc_bench/$c $OUT/pmc_$c.json > /dev/null && echo "pmc $c summarized"
+        case $c in c3_up) D="2048 16384 4096";; c3_down) D="2048 4096 16384";; c4_shard) D="8192 4096 4096";; *) D="4096 4096 4096";; esac
+        python3 scripts/summarize_pmc.py gpurun_out/pmc_bench/$c $OUT/pmc_$c.json $D > /dev/null && echo "pmc $c summarized"
       done ;;
   esac
 done
