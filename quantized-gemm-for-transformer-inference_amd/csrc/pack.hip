@@ -350,12 +350,26 @@ __global__ __launch_bounds__(256) void pack_rows_block_kernel(const float *__res
     pack_row_block_body(xcd_contig(blockIdx.x, 0, gridDim.x), src, sh, rows, len, range, scale, q, rows_pad, k_pad, red);
 }
 
+// R > 0 (rows of <= 4096 floats): 8 rows per 512-thread block, one wave per row, staged in LDS and written out
+// as whole 128-B lines of the fragment-major q (a line = 16-B pieces of 8 rows).  R == 0 (streaming rows): 4
+// rows per 256-thread block, stored directly.
 template <int R>
-__global__ __launch_bounds__(256) void pack_rows_vec_kernel(const float *__restrict__ src, int64_t sh, int rows,
-                                                            int len, float range, float *__restrict__ scale,
-                                                            int8_t *__restrict__ q, int64_t rows_pad,
-                                                            int64_t k_pad) {
-    pack_rows_vec_body<R>(xcd_contig(blockIdx.x, 0, gridDim.x), src, sh, rows, len, range, scale, q, rows_pad, k_pad);
+__global__ __launch_bounds__(R > 0 ? 512 : 256) void pack_rows_vec_kernel(const float *__restrict__ src, int64_t sh,
+                                                                          int rows, int len, float range,
+                                                                          float *__restrict__ scale,
+                                                                          int8_t *__restrict__ q, int64_t rows_pad,
+                                                                          int64_t k_pad) {
+    const int b = xcd_contig(blockIdx.x, 0, gridDim.x);
+    if constexpr (R > 0) {
+        __shared__ __attribute__((aligned(16))) uint32_t xstage[8 * kStageRowWordsMax];
+        const int rsw = (int)(k_pad >> 2) + 16;
+        pack_rows_vec_body<R, false, false, true>(2 * (int64_t)b, src, sh, rows, len, range, scale, q, rows_pad, k_pad,
+                                                  nullptr, xstage + (threadIdx.x >> 6) * rsw);
+        __syncthreads();
+        write_staged_rows<8>(xstage, rsw, q, 8 * (int64_t)b, k_pad);
+    } else {
+        pack_rows_vec_body<R>(b, src, sh, rows, len, range, scale, q, rows_pad, k_pad);
+    }
 }
 
 // pack_rows, generic strides (any sh, sw): scalar loads, two passes.
@@ -1074,7 +1088,9 @@ hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, 
                                                              out.rows_pad, out.k_pad);
         return hipGetLastError();
     }
-#define QG_ROWS(Rv) pack_rows_vec_kernel<Rv><<<grid, block, 0, stream>>>(src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad)
+#define QG_ROWS(Rv)                                                                                               \
+    pack_rows_vec_kernel<Rv><<<(Rv) > 0 ? (unsigned)(out.rows_pad / 8) : grid.x, (Rv) > 0 ? 512 : 256, 0, stream>>>( \
+        src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad)
     if (rows_regs(len) < 0) {
         pack_rows_block_kernel<<<(unsigned)out.rows_pad, 256, 0, stream>>>(src, sh, rows, len, range, out.scale, out.q,
                                                                            out.rows_pad, out.k_pad);
