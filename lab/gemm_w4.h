@@ -30,7 +30,8 @@ namespace qgemm {
 namespace gemm {
 
 enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4PadT = 16, kW4RowMajor = 32, kW4NoA = 64,
-               kW4NoB = 128, kW4K1 = 256, kW4K4 = 512, kW4Sync = 1024 };
+               kW4NoB = 128, kW4K1 = 256, kW4K4 = 512, kW4Sync = 1024,
+               kW4Nt = 2048, kW4NoPrio = 4096 };
 
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_w4_stamp[4096 * 6];
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
         un = un < nsub ? un : nsub - 1;
         if constexpr (kFlags & kW4K1) un = 0;   // ablation: every load re-reads sub-step 0 (L1 / L2 hits)
         if constexpr (kFlags & kW4K4) un &= 3;  // ablation: 4 sub-steps cycled (L2 hits)
-        __builtin_amdgcn_s_setprio(1);
+        if constexpr (!(kFlags & kW4NoPrio)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (!(kFlags & kW4NoPrio)) __builtin_amdgcn_s_setprio(0);
     };
 #pragma unroll
     for (int j = 0; j < 16; ++j) ld(a0, b0, j, 0, true);
@@ -604,7 +605,13 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
             for (int it = 0; it < 32; ++it) {
                 const int rr = 2 * it + (lane >> 5);
                 const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
-                *reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4) = v;
+                float4 *dst = reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4);
+                if constexpr (kFlags & kW4Nt) {
+                    typedef float v4f __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f *>(dst));
+                } else {
+                    *dst = v;
+                }
             }
         } else {
             for (int it = 0; it < 32; ++it) {

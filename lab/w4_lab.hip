@@ -69,6 +69,8 @@ int main(int argc, char **argv) {
         {"f4_noB_ns", gemm_i8_f4<kW4NoStore | kW4NoB>, 256, true},
         {"f4_k1_ns", gemm_i8_f4<kW4NoStore | kW4K1>, 256, true},
         {"f4sync", gemm_i8_f4<kW4Sync>, 256, true},
+        {"f4nt", gemm_i8_f4<kW4Nt>, 256, true},
+        {"f4noprio", gemm_i8_f4<kW4NoPrio>, 256, true},
         {"f4sync_nostore", gemm_i8_f4<kW4Sync | kW4NoStore>, 256, true},
         {"f4_k4_ns", gemm_i8_f4<kW4NoStore | kW4K4>, 256, true},
     };

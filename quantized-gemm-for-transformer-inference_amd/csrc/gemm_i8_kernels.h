@@ -1027,7 +1027,9 @@ __device__ __forceinline__ bool splitk_arrive_fm(const GemmArgs &p, unsigned *la
     return *last == (unsigned)(S - 1);
 }
 
-template <int kEpi = kEpiNone, bool kI32 = false, bool kSplit = false>
+// kNtC: the full-tile output stores are nontemporal (C2 bench, one box, interleaved: 11 598 vs 11 431 GEMMs/s, GEMM
+// 58.2 vs 59.5 us by events; profiles/r03_ab_nt_c.log) -- the 64-MiB tail streams past the caches
+template <int kEpi = kEpiNone, bool kI32 = false, bool kSplit = false, bool kNtC = !kI32>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
@@ -1189,7 +1191,13 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
             for (int it = 0; it < 32; ++it) {
                 const int rr = 2 * it + (lane >> 5);
                 const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
-                *reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4) = v;
+                float4 *dst = reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4);
+                if constexpr (kNtC) {
+                    typedef float v4f __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f *>(dst));
+                } else {
+                    *dst = v;
+                }
             }
         } else {
             for (int it = 0; it < 32; ++it) {
