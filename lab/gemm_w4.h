@@ -31,7 +31,7 @@ namespace gemm {
 
 enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4PadT = 16, kW4RowMajor = 32, kW4NoA = 64,
                kW4NoB = 128, kW4K1 = 256, kW4K4 = 512, kW4Sync = 1024,
-               kW4Nt = 2048, kW4NoPrio = 4096 };
+               kW4Nt = 2048, kW4NoPrio = 4096, kW4Direct = 8192 };
 
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_w4_stamp[4096 * 6];
@@ -581,6 +581,25 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
     float cwv[8];
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) cwv[ni] = sCw[c0 + ni * 16 + lrow];
+    if constexpr (kFlags & kW4Direct) {
+        // ablation: dequantized straight from the accumulators, dword nontemporal stores (4 rows x 64 B per
+        // wave instruction), no LDS image (full tiles only)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            float cx4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cx4[r] = sCx[r0 + mi * 16 + 4 * kq + r];
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    __builtin_nontemporal_store(
+                        dequantize(acc[mi][ni][r], outer_product(cx4[r], cwv[ni]), p.inv_r2),
+                        C + (int64_t)(gi0 + r0 + mi * 16 + 4 * kq + r) * p.csh + gj0 + c0 + ni * 16 + lrow);
+        }
+        stamp(2);
+        return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         float cxv[4][4];

@@ -71,6 +71,7 @@ int main(int argc, char **argv) {
         {"f4sync", gemm_i8_f4<kW4Sync>, 256, true},
         {"f4nt", gemm_i8_f4<kW4Nt>, 256, true},
         {"f4noprio", gemm_i8_f4<kW4NoPrio>, 256, true},
+        {"f4direct", gemm_i8_f4<kW4Direct>, 256, true},
         {"f4sync_nostore", gemm_i8_f4<kW4Sync | kW4NoStore>, 256, true},
         {"f4_k4_ns", gemm_i8_f4<kW4NoStore | kW4K4>, 256, true},
     };

@@ -191,6 +191,19 @@ def test_split_k_shapes_share_library_scratch(qg, oracle, device):
         assert_bits_equal(O.cpu().numpy(), want, f"call {i}: {M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N,K", [(4000, 4100, 1000), (3900, 2600, 700), (4096, 2610, 100), (3333, 4095, 800)])
+def test_256_tile_kernel_ragged_shapes(qg, oracle, device, M, N, K):
+    """>= 160 tiles of 256 x 256 (gemm_i8_fm, no split): ragged M and N (partial edge tiles take the guarded
+    store path), and K padded to 2 / 12 / 14 / 16 sub-steps of 64 (the main loop's 3-sub-step unroll leaves
+    rest 2 / 0 / 2 / 1, and at 2 sub-steps it never runs)."""
+    L = qg.load()
+    tile = ctypes.c_int(0)
+    assert L.qgemm_gemm_plan(M, N, K, ctypes.byref(tile), None) == 1 and tile.value == 256
+    X, W = oracle.inputs(M, N, K, 141)
+    X[::9, 0] = -1.25
+    assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 4096, 2048), (1900, 4000, 3000), (1800, 4096, 4500)])
 def test_256_tile_split_k_plans(qg, oracle, device, M, N, K):
     """128 tiles of 256 x 256 with K >= 2048: the split-K plan (S = 2) on gemm_i8_fm -- slabs stored
