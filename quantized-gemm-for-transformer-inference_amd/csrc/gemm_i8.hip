@@ -147,7 +147,7 @@ static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const 
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     if (kEpi == kEpiOutlier || (p.splits > 1 && (g_split_kernel == 1 || p.splits != 2)))
-        return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF>);
+        return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF | kPPNtStore>);
     if constexpr (kEpi != kEpiOutlier) {
         if (p.splits > 1) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, true>);
         return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);

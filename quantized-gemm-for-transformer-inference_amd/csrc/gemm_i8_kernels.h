@@ -316,6 +316,19 @@ __device__ __forceinline__ float epi_extra(float o, const float *sB, int jl) {
 // serves the 8 rows.  Columns past n read wo's padding and are never stored.
 // sX [256 tile rows][8] / sW [8][256 tile cols]: the staged xo / wo values when ocnt <= kOutlierStaged
 // (nullptr otherwise); gi0 = the tile's first row.
+// a 16-B output store, nontemporal when kNt (the 64-MiB output streams past the caches: the next launch's
+// inputs are not evicted by it)
+template <bool kNt>
+__device__ __forceinline__ void st_f4(float *dst, float4 v) {
+    if constexpr (kNt) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f *>(dst));
+    } else {
+        *reinterpret_cast<float4 *>(dst) = v;
+    }
+}
+
+template <bool kNt = false>
 __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const float *T, int i0, int gj0, int c4,
                                                       int tid, bool full, const float *sX, const float *sW,
                                                       int gi0) {
@@ -354,7 +367,7 @@ __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const f
                 const float vv[4] = {__fadd_rn(o.x, c[g][0]), __fadd_rn(o.y, c[g][1]), __fadd_rn(o.z, c[g][2]),
                                      __fadd_rn(o.w, c[g][3])};
                 if (full) {
-                    *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+                    st_f4<kNt>(C + (int64_t)i * p.csh + j, make_float4(vv[0], vv[1], vv[2], vv[3]));
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
@@ -408,7 +421,7 @@ __device__ __forceinline__ void epilogue_outlier_half(const GemmArgs &p, const f
             const float vv[4] = {__fadd_rn(o.x, c[g][0]), __fadd_rn(o.y, c[g][1]), __fadd_rn(o.z, c[g][2]),
                                  __fadd_rn(o.w, c[g][3])};
             if (full) {
-                *reinterpret_cast<float4 *>(C + (int64_t)i * p.csh + j) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+                st_f4<kNt>(C + (int64_t)i * p.csh + j, make_float4(vv[0], vv[1], vv[2], vv[3]));
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
@@ -514,7 +527,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs &p, int8_t *lds, v4i (
             const int c4 = (tid & 63) * 4;
             if constexpr (kEpi == kEpiOutlier) {
                 if (*p.ocount > 0) {
-                    epilogue_outlier_half(p, T, gi0 + half * 128, gj0, c4, tid, full, staged ? sX : nullptr, sW,
+                    epilogue_outlier_half<kNt>(p, T, gi0 + half * 128, gj0, c4, tid, full, staged ? sX : nullptr, sW,
                                           gi0);
                     continue;
                 }
