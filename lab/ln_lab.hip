@@ -83,17 +83,26 @@ int main(int argc, char **argv) {
         printf("vector vs scalar kernel: Y %s  q %s  scale %s\n", same(Y2, Y3, (size_t)rows * w * 4),
                same(v.q, v2.q, v.rows_pad * v.k_pad), same(v.scale, v2.scale, v.rows_pad * 4));
         hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-        for (int var = 0; var < 2; ++var) {
+        if (w <= 1024) {  // the LDS-walking chain in the same register-resident kernel
+            add_layernorm_rows_vec_kernel<true, 4, 0, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, sizeof(float) * 4 * w>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+            CK(hipDeviceSynchronize());
+            printf("hop chain vs LDS chain: Y %s  q %s  scale %s\n", same(Y2, Y3, (size_t)rows * w * 4),
+                   same(v.q, v2.q, v.rows_pad * v.k_pad), same(v.scale, v2.scale, v.rows_pad * 4));
+        }
+        for (int var = 0; var < 3; ++var) {
+            if (var == 2 && w > 1024) break;
             std::vector<float> ts;
             for (int it = 0; it < 30; ++it) {
                 CK(hipEventRecord(e0));
                 if (var == 0) CK(launch_add_layernorm_rows_pack(A, B, Y2, rows, w, 127.0f, v, nullptr));
+                else if (var == 2) add_layernorm_rows_vec_kernel<true, 4, 0, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, sizeof(float) * 4 * w>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
                 else add_layernorm_rows_kernel<true><<<(unsigned)((v2.rows_pad + 3) / 4), 256, lds>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
                 CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
                 float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms * 1000);
             }
             std::sort(ts.begin(), ts.end());
-            printf("%s kernel: median %.2f us\n", var ? "scalar" : "vector", ts[ts.size() / 2]);
+            const char *nm[3] = {"vector (hop chain)", "scalar", "vector (LDS chain)"};
+            printf("%s kernel: median %.2f us\n", nm[var], ts[ts.size() / 2]);
         }
     }
     // phase stamps (s_memrealtime, 100 MHz) of the fused kernel, medians over rows
@@ -105,7 +114,7 @@ int main(int argc, char **argv) {
         CK(hipDeviceSynchronize());
         static unsigned long long st[4096][8];
         CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_ln_stamp), sizeof(st)));
-        const char *names[6] = {"load a+b", "mean chain", "d^2 stage", "var chain", "y loop", "pack"};
+        const char *names[6] = {"load a+b", "mean chain", "d^2", "var chain", "y loop", "pack"};
         unsigned long long t0 = ~0ull, t1 = 0;
         for (int r = 0; r < rows && r < 4096; ++r) { t0 = std::min(t0, st[r][0]); t1 = std::max(t1, st[r][6]); }
         for (int ph = 0; ph < 6; ++ph) {

@@ -198,28 +198,39 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 4))
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's exps are in LDS
     __builtin_amdgcn_wave_barrier();
     stamp(6);
-    float sum = 0.0f;
-    if (lane < 2 && wave * 2 + lane < rows && !(kSkip & 8)) {
-        const float *srow = S + (wave * 2 + lane) * kSStride;
-        int c = 0;
-        for (; c + 64 <= seq; c += 64) {  // 16 LDS reads in flight per group of 64 adds
-            float4 v[16];
+    // the two sums at once, each hopping lane to lane (hop_left): row 2w in lanes 0-31, row 2w+1 in lanes
+    // 32-63, lane h of a half holding elements 16h .. 16h+15 of its row in registers; after step t the
+    // chain through lane h = t - 1 of each half sits in that lane (lane 32 starts from lane 31's initial
+    // zero; both halves run the same instructions).  Elements past seq are -0.0f, which leaves any sum
+    // unchanged, so the last lane's 16 adds stay uniform.  Per element one dependent add, no LDS reads
+    // inside the chain (the LDS-walking form exposed one read latency per 64 elements).
+    float sum_a = 0.0f, sum_b = 0.0f;
+    if (!(kSkip & 8)) {
+        const int hl = lane & 31, nl = (seq + 15) >> 4;  // lanes per half that hold elements (nl <= 32)
+        const float *srow = S + (wave * 2 + (lane >> 5)) * kSStride + 16 * hl;
+        float e[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = *reinterpret_cast<const float4 *>(srow + c + 4 * j);
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                sum = __fadd_rn(sum, v[j].x);
-                sum = __fadd_rn(sum, v[j].y);
-                sum = __fadd_rn(sum, v[j].z);
-                sum = __fadd_rn(sum, v[j].w);
-            }
+        for (int j = 0; j < 4; ++j) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (hl < nl && wave * 2 + (lane >> 5) < rows) v = *reinterpret_cast<const float4 *>(srow + 4 * j);
+            e[4 * j] = v.x; e[4 * j + 1] = v.y; e[4 * j + 2] = v.z; e[4 * j + 3] = v.w;
         }
-        for (; c < seq; ++c) sum = __fadd_rn(sum, srow[c]);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (16 * hl + j >= seq) e[j] = -0.0f;
+        float s = 0.0f;
+        for (int t = 0; t < nl; ++t) {
+            s = __fadd_rn(hop_left(s), e[0]);
+#pragma unroll
+            for (int j = 1; j < 16; ++j) s = __fadd_rn(s, e[j]);
+        }
+        sum_a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), nl - 1));
+        sum_b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 32 + nl - 1));
     }
     stamp(7);
     for (int rr = 0; rr < 2 && !(kSkip & 2); ++rr) {
         const int rl = wave * 2 + rr;
-        const float srr = __shfl(sum, rr, 64);
+        const float srr = rr == 0 ? sum_a : sum_b;
         if (rl >= rows) break;
         float *srow = S + rl * kSStride;
         for (int c = lane; c < seq; c += 64) srow[c] = __fdiv_rn(srow[c], srr);

@@ -48,6 +48,40 @@ __device__ __forceinline__ float seq_sum(const float *row, int w) {
     return sum;
 }
 
+// The same sequential fp32 sum over a row held in registers: element 4(l + 64 i) + c is x[i].c of lane l
+// (the layout of add_layernorm_rows_vec_kernel), w4 = w / 4 float4 columns.  The running sum hops from
+// lane to lane: every step is one v_add_f32 whose first operand is the LEFT neighbour's sum (DPP
+// wave_ror:1: lane l reads lane l - 1, lane 0 reads lane 63), then three in-lane adds.  Every lane runs
+// every step, so after step t of group i lane t - 1 holds the chain through its own four elements
+// (induction: each step extends the chain that had reached the left neighbour one step earlier), and lane 63
+// hands a full group on to lane 0 of the next.  Per element one dependent add and no LDS round trip: the
+// LDS-walking chain (seq_sum) spends ~7-8 cycles per element waiting on its ds_read groups.  The result is
+// the sum in lane (w4 - 1) mod 64, broadcast.
+__device__ __forceinline__ float hop_step(float s, const float4 &v) {
+    s = __fadd_rn(hop_left(s), v.x);
+    s = __fadd_rn(s, v.y);
+    s = __fadd_rn(s, v.z);
+    return __fadd_rn(s, v.w);
+}
+template <int kV>
+__device__ __forceinline__ float lane_chain_sum(const float4 (&x)[kV], int w4) {
+    float s = 0.0f;
+    int last = 63;
+#pragma unroll
+    for (int i = 0; i < kV; ++i) {
+        const int n = w4 - 64 * i < 64 ? w4 - 64 * i : 64;
+        if (n <= 0) break;
+        int t = 0;
+        for (; t + 8 <= n; t += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = hop_step(s, x[i]);
+        }
+        for (; t < n; ++t) s = hop_step(s, x[i]);
+        last = n - 1;
+    }
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), last));
+}
+
 // fl((x - mean)^2): pow(x - mean, 2) as fp32 d*d (CUDA's float pow(float, int) overload)
 __device__ __forceinline__ float sq_dev(float x, float mean) {
     const float d = __fsub_rn(x, mean);
@@ -171,7 +205,9 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
 // columns 4j..4j+3 (j = lane + 64 i, i < kV) in registers from the first load to the last use, so
 // neither the normalisation nor the pack re-reads A, B or LDS; each packed dword is
 // one lane's four columns.
-template <bool kPack, int kV, int kStamp = 0>
+// kHop (the product): both sums as lane_chain_sum over the registers; false: staged in LDS and walked by
+// seq_sum (lab comparison)
+template <bool kPack, int kV, int kStamp = 0, bool kHop = true>
 __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     const float *__restrict__ A, const float *__restrict__ B, float *__restrict__ Y, int64_t rows, int w,
     int8_t *__restrict__ q, float *__restrict__ qscale, int64_t k_pad, int64_t rows_pad, float range) {
@@ -198,33 +234,46 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
 #pragma unroll
     for (int i = 0; i < kV; ++i) {
         const int j = lane + 64 * i;
+        x[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (j < w4) {
             const float4 av = a[j], bv = b[j];
             x[i] = make_float4(__fadd_rn(av.x, bv.x), __fadd_rn(av.y, bv.y), __fadd_rn(av.z, bv.z),
                                __fadd_rn(av.w, bv.w));  // op_add (transformer.cu:58)
-            reinterpret_cast<float4 *>(st)[j] = x[i];
+            if constexpr (!kHop) reinterpret_cast<float4 *>(st)[j] = x[i];
         }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (!kHop) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
     stamp(1);
     const float fw = (float)w;
-    const float mean = __fdiv_rn(seq_sum(st, w), fw);           // op_layernorm.cuh:15-19
+    const float mean = __fdiv_rn(kHop ? lane_chain_sum<kV>(x, w4) : seq_sum(st, w), fw);  // op_layernorm.cuh:15-19
     stamp(2);
-    __builtin_amdgcn_wave_barrier();
-    // the squared deviations replace the row in LDS, formed from the registers (a chain that formed
-    // them itself would carry the sub -> mul latency on every add: measured 2x slower)
+    // the squared deviations, formed from the registers (a chain that formed them itself would carry the
+    // sub -> mul latency on every add: measured 2x slower)
+    float var;
+    if constexpr (kHop) {
+        float4 d[kV];
 #pragma unroll
-    for (int i = 0; i < kV; ++i) {
-        const int j = lane + 64 * i;
-        if (j < w4)
-            reinterpret_cast<float4 *>(st)[j] =
-                make_float4(sq_dev(x[i].x, mean), sq_dev(x[i].y, mean), sq_dev(x[i].z, mean), sq_dev(x[i].w, mean));
+        for (int i = 0; i < kV; ++i)
+            d[i] = make_float4(sq_dev(x[i].x, mean), sq_dev(x[i].y, mean), sq_dev(x[i].z, mean), sq_dev(x[i].w, mean));
+        stamp(3);
+        var = __fdiv_rn(lane_chain_sum<kV>(d, w4), fw);            // :21-25
+    } else {
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < kV; ++i) {
+            const int j = lane + 64 * i;
+            if (j < w4)
+                reinterpret_cast<float4 *>(st)[j] =
+                    make_float4(sq_dev(x[i].x, mean), sq_dev(x[i].y, mean), sq_dev(x[i].z, mean), sq_dev(x[i].w, mean));
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        stamp(3);
+        var = __fdiv_rn(seq_sum(st, w), fw);                       // :21-25
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    stamp(3);
-    const float var = __fdiv_rn(seq_sum(st, w), fw);            // :21-25
     stamp(4);
     float cand = -INFINITY;
 #pragma unroll
@@ -271,7 +320,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
 template <bool kPack>
 hipError_t launch_ln_vec(const float *A, const float *B, float *Y, int64_t rows, int w, int8_t *q, float *qscale,
                          int64_t k_pad, int64_t rows_pad, float range, int64_t grid_rows, hipStream_t stream) {
-    const size_t lds = sizeof(float) * kRowWaves * w;
+    const size_t lds = 0;  // the sums run in registers (kHop)
     const unsigned grid = (unsigned)((grid_rows + kRowWaves - 1) / kRowWaves);
     if (w <= 1024)
         add_layernorm_rows_vec_kernel<kPack, 4><<<grid, 64 * kRowWaves, lds, stream>>>(A, B, Y, rows, w, q, qscale, k_pad,

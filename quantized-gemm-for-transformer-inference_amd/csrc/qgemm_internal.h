@@ -99,6 +99,13 @@ __device__ __forceinline__ float dequantize(int acc, float outer, float inv_r2) 
     return __fmul_rn(__fmul_rn((float)acc, outer), inv_r2);
 }
 
+// The running value of the lane to the LEFT (DPP wave_ror:1: lane l reads lane l - 1, lane 0 reads lane 63),
+// for sequential fp32 sums that hop from lane to lane (encoder_ops.hip lane_chain_sum, attention.hip).  With
+// old = 0 and bound_ctrl set, hipcc folds the move into the consuming v_add_f32 (v_add_f32_dpp).
+__device__ __forceinline__ float hop_left(float s) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x13C /* wave_ror:1 */, 0xf, 0xf, true));
+}
+
 // Counter-based generator shared with oracle_uniform_at (oracle/qgemm_oracle.c).
 __host__ __device__ inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
