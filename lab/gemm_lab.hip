@@ -220,6 +220,11 @@ int main(int argc, char **argv) {
             {"t64d8_S1", gemm_i8_small<64, 0, 8>, 64, 1}, {"t64d8_S2", gemm_i8_small<64, 0, 8>, 64, 2},
             {"t32d2_S1", gemm_i8_small<32>, 32, 1}, {"t32d3_S1", gemm_i8_small<32, 0, 3>, 32, 1},
             {"t32d4_S1", gemm_i8_small<32, 0, 4>, 32, 1},
+            // direct-load small tiles (gemm_i8_sd<TB, KW, D>)
+            {"sd64k1d4", gemm_i8_sd<64, 1, 4>, 64, 1}, {"sd64k1d8", gemm_i8_sd<64, 1, 8>, 64, 1},
+            {"sd64k4d4", gemm_i8_sd<64, 4, 4>, 64, 1}, {"sd64k4d6", gemm_i8_sd<64, 4, 6>, 64, 1},
+            {"sd32k1d8", gemm_i8_sd<32, 1, 8>, 32, 1}, {"sd32k4d4", gemm_i8_sd<32, 4, 4>, 32, 1},
+            {"sd32k4d8", gemm_i8_sd<32, 4, 8>, 32, 1}, {"sd32k4d12", gemm_i8_sd<32, 4, 12>, 32, 1},
         };
         auto args = [&](const SV &v, float *out) {
             GemmArgs q = p; q.C = out; q.splits = v.S; q.slabs = slabs; q.tickets = tick; q.reset_tickets = 1;
