@@ -340,8 +340,11 @@ def c4_node(args, qg, dev, world, rank, distributed):
 def gemm_kernel_name(L, M, N, K, outlier):
     """The GEMM kernel this call launches, as the library plans it (qgemm_gemm_plan)."""
     if outlier:
-        return ("gemm_i8_pp<2, kEpiOutlier> (256x256 tiles, 8 waves ping-pong, LDS-DMA ring, fused dequant + "
-                "outlier fp32 chain)")
+        if os.environ.get("QGEMM_OUTLIER_KERNEL", "").startswith("p"):
+            return ("gemm_i8_pp<2, kEpiOutlier> (256x256 tiles, 8 waves ping-pong, LDS-DMA ring, fused dequant + "
+                    "outlier fp32 chain on VALU)")
+        return ("gemm_i8_fm<kEpiOutlier> (256x256 tiles, 4 waves of 128x128, fragment-major operands straight to "
+                "VGPRs, fused dequant + outlier fp32 chain on f32 MFMAs)")
     tile, name = ctypes.c_int(0), ctypes.c_char_p()
     splits = L.qgemm_gemm_plan(M, N, K, ctypes.byref(tile), ctypes.byref(name))
     return f"{name.value.decode()}, plan: {tile.value}-tiles x {splits} K-slice(s)"

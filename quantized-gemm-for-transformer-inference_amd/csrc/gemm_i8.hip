@@ -23,6 +23,12 @@ static const int g_split_kernel = [] {
     const char *e = getenv("QGEMM_SPLIT_KERNEL");
     return e && e[0] == 'p' ? 1 : 0;
 }();
+// the LLM.int8() outlier epilogue: 0 = gemm_i8_fm with the chain on f32 MFMAs (product), 1 = the ping-pong
+// kernel's VALU chain (QGEMM_OUTLIER_KERNEL=pp: A/B)
+static const int g_outlier_kernel = [] {
+    const char *e = getenv("QGEMM_OUTLIER_KERNEL");
+    return e && e[0] == 'p' ? 1 : 0;
+}();
 static int g_event_mode = 0;  // 0: hipExtLaunchKernel events, 1: hipEventRecord around the launch
 void set_gemm_event_mode(int mode) { g_event_mode = mode; }
 void set_gemm_events(hipEvent_t start, hipEvent_t stop) { t_events = GemmEvents{start, stop}; }
@@ -146,13 +152,14 @@ static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const 
 
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
-    if (kEpi == kEpiOutlier || (p.splits > 1 && (g_split_kernel == 1 || p.splits != 2)))
+    if (kEpi == kEpiOutlier && g_outlier_kernel == 1)  // QGEMM_OUTLIER_KERNEL=pp: the ping-pong kernel's VALU chain
+        return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF | kPPNtStore>);
+    if (p.splits > 1 && (g_split_kernel == 1 || p.splits != 2))
         return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF | kPPNtStore>);
     if constexpr (kEpi != kEpiOutlier) {
         if (p.splits > 1) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, true>);
-        return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);
     }
-    return hipErrorNotSupported;
+    return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);
 }
 
 template <int TB, int kEpi, int kDepth>

@@ -1046,6 +1046,7 @@ template <int kEpi = kEpiNone, bool kI32 = false, bool kSplit = false, bool kNtC
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
+    static_assert(!(kEpi == kEpiOutlier && kSplit), "the outlier epilogue runs on unsplit plans");
     constexpr int TS = 132;                 // padded row of a wave's epilogue block (conflict-free ds_write)
     constexpr int kBlockBytes = 64 * TS * 4;
     __shared__ __attribute__((aligned(16))) int8_t lds[4 * kBlockBytes + 2048 + 16];
@@ -1073,6 +1074,9 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         const_cast<int8_t *>(uniform_ptr(p.B + (((int64_t)tn * 16 + wn * 8) * nsub + u0) * 1024)), 0,
         __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
     const int voff = lane * 16;
+    // kEpiOutlier: the outlier-column count (device-side), read before the k-loop so the epilogue's operand
+    // loads do not wait on it
+    const int ocnt = kEpi == kEpiOutlier ? __builtin_amdgcn_readfirstlane(*p.ocount) : 0;
 
     v4i acc[8][8];
 #pragma unroll
@@ -1135,6 +1139,26 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     const int gi0 = tm * BM, gj0 = tn * BN;
     const int lrow = lane & 15, kq = lane >> 4;
     const int r0 = wm * 128, c0 = wn * 128;
+    // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) for both halves, loaded
+    // together here so their latency is paid once: ow[step][ni] = wo[t][col], ox[half][mq][step] = xo[row][t]
+    // with t = 4 step + kq; +0 / -0 past the count (see below)
+    float ox[2][4][2], ow[2][8];
+    if constexpr (kEpi == kEpiOutlier) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const int t = 4 * tt + kq;
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+                ow[tt][ni] = t < ocnt ? p.wo[(int64_t)t * p.wo_ld + gj0 + c0 + ni * 16 + lrow] : -0.0f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int mq = 0; mq < 4; ++mq) {
+                    const int i = gi0 + r0 + 64 * h + mq * 16 + lrow;
+                    ox[h][mq][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * ocnt + t] : 0.0f;
+                }
+        }
+    }
     float *sCx = reinterpret_cast<float *>(lds + 4 * kBlockBytes);
     float *sCw = sCx + BM;
     if constexpr (!kI32) {
@@ -1176,6 +1200,46 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         for (int mq = 0; mq < 4; ++mq)
 #pragma unroll
             for (int r = 0; r < 4; ++r) cxv[mq][r] = kI32 ? 0.0f : sCx[r0 + 64 * s + mq * 16 + 4 * kq + r];
+        if constexpr (kEpi == kEpiOutlier) {
+            // O = fl(O8 + Co), Co = the fp32 chain over the outlier columns from +0 in ascending t of
+            // xo[i][t] * wo[t][j], on v_mfma_f32_16x16x4_f32 (its result is that k-ordered chain bit for bit,
+            // as in the fp32 GEMMs): 4 columns per MFMA, D laid out as the int32 accumulators, one 16-row
+            // block of the half at a time.  A step past the count multiplies +0 by -0: fma(+0, -0, c) = c for
+            // every c, -0 included (+0 * +0 would turn a -0 sum into +0).
+            // The first 8 columns' operands were loaded once, ahead of both halves (ox / ow); columns past 8
+            // load per step.
+            typedef float v4f_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq) {
+                v4f_t oc[8];
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni) oc[ni] = v4f_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+                    if (4 * tt < ocnt)
+#pragma unroll
+                        for (int ni = 0; ni < 8; ++ni)
+                            oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(ox[s][mq][tt], ow[tt][ni], oc[ni], 0, 0, 0);
+                const int ia = gi0 + r0 + 64 * s + mq * 16 + lrow;  // the A-operand row of this lane
+#pragma unroll 1
+                for (int t0 = 8; t0 < ocnt; t0 += 4) {
+                    const int t = t0 + kq;  // the lane's k within the MFMA step
+                    const float xa = t < ocnt && ia < p.m ? p.xo[(int64_t)ia * ocnt + t] : 0.0f;
+                    float wb[8];
+#pragma unroll
+                    for (int ni = 0; ni < 8; ++ni)
+                        wb[ni] = t < ocnt ? p.wo[(int64_t)t * p.wo_ld + gj0 + c0 + ni * 16 + lrow] : -0.0f;
+#pragma unroll
+                    for (int ni = 0; ni < 8; ++ni) oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, wb[ni], oc[ni], 0, 0, 0);
+                }
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        T[(mq * 16 + 4 * kq + r) * TS + ni * 16 + lrow] = __fadd_rn(
+                            dequantize(acc[4 * s + mq][ni][r], outer_product(cxv[mq][r], cwv[ni]), p.inv_r2), oc[ni][r]);
+            }
+        } else {
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) {
             const int jl = ni * 16 + lrow;
@@ -1195,6 +1259,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
                     }
                     T[il * TS + jl] = o;
                 }
+        }
         }
         // the wave's own block: its ds_writes precede its ds_reads (one wave's LDS ops stay in order)
         const int c4 = (lane & 31) * 4;

@@ -64,6 +64,30 @@ def test_outlier_fast_path_nan_and_none(qg, oracle, device):
     assert_bits_equal(C.cpu().numpy(), want, "fast path, NaN column")
 
 
+@pytest.mark.parametrize("ncols", [1, 3])
+def test_outlier_chain_keeps_negative_zero(qg, oracle, device, ncols):
+    """An outlier chain that underflows to -0 added to an int8 part that is -0: O = fl(-0 + -0) = -0.  The GEMM
+    epilogue runs the chain on 4-column f32 MFMA steps, so a count that is not a multiple of 4 pads the last
+    step -- with +0 * -0, which leaves a -0 sum alone (+0 * +0 would give +0).  O8[5, 11] is -0: acc < 0 times
+    an outer product Cx * Cw that underflows to +0."""
+    M, N, K = 2560, 4096, 128  # the fast path: 160 256-tiles
+    X, W = oracle.inputs(M, N, K, 12)
+    cols = [7, 40, 90][:ncols]
+    X[5, :] = 0.0
+    X[5, 1] = 1e-22           # Cx[5] = 1e-22, q = 127
+    W[:, 11] = 0.0
+    W[1, 11] = -1e-25         # Cw[11] = 1e-25, q = -127: acc[5, 11] = -16129, fl(Cx * Cw) = +0
+    for c in cols:
+        X[100, c] = 50.0      # makes column c an outlier column
+        X[5, c] = -1e-30
+        W[c, 11] = 1e-30      # -1e-30 * 1e-30 underflows to -0
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    assert cnt == wcnt == ncols
+    assert want[5, 11] == 0.0 and np.signbit(want[5, 11]), "the oracle's value is -0"
+    assert_bits_equal(C.cpu().numpy(), want, f"outlier chain -0, {ncols} columns")
+
+
 def test_no_outliers_is_the_plain_path(qg, oracle, device):
     X, W = oracle.inputs(256, 300, 700, 6)
     C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
