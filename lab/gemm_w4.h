@@ -31,7 +31,7 @@ namespace gemm {
 
 enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4PadT = 16, kW4RowMajor = 32, kW4NoA = 64,
                kW4NoB = 128, kW4K1 = 256, kW4K4 = 512, kW4Sync = 1024,
-               kW4Nt = 2048, kW4NoPrio = 4096, kW4Direct = 8192 };
+               kW4Nt = 2048, kW4NoPrio = 4096, kW4Direct = 8192, kW4Rot = 16384 };
 
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_w4_stamp[4096 * 6];
@@ -600,6 +600,9 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
         stamp(2);
         return;
     }
+    // kW4Rot: each tile starts its row-pair loop at its own offset (spreading the rows written at one time
+    // over the chip; profiles/r03_f4_store_order_lab.log)
+    const int rot = (kFlags & kW4Rot) ? ((tn * 7 + tm * 3) & 31) : 0;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         float cxv[4][4];
@@ -622,7 +625,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
         if (full && rows_full) {
 #pragma unroll 8
             for (int it = 0; it < 32; ++it) {
-                const int rr = 2 * it + (lane >> 5);
+                const int rr = 2 * ((it + rot) & 31) + (lane >> 5);
                 const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
                 float4 *dst = reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4);
                 if constexpr (kFlags & kW4Nt) {

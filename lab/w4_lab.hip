@@ -76,6 +76,43 @@ int main(int argc, char **argv) {
         {"f4_k4_ns", gemm_i8_f4<kW4NoStore | kW4K4>, 256, true},
     };
     dim3 grid(p.tiles_m * p.tiles_n);
+    // stride mode: the product-form kernel (nontemporal stores) with the output row stride n vs n + 32 / n + 64
+    // floats -- does the epilogue's store pattern pay for a power-of-two row stride?
+    if (only && std::string(only) == "stride") {
+        float *Cp; CK(hipMalloc(&Cp, (size_t)m * (n + 64) * 4));
+        struct SV { const char *name; KernelFn fn; int pad; };
+        constexpr int NV = 4;
+        const SV sv[NV] = {{"f4nt", gemm_i8_f4<kW4Nt>, 0}, {"f4nt pad32", gemm_i8_f4<kW4Nt>, 32},
+                           {"f4nt pad64", gemm_i8_f4<kW4Nt>, 64}, {"f4nt rot", gemm_i8_f4<kW4Nt | kW4Rot>, 0}};
+        hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        std::vector<std::vector<float>> t(NV);
+        dim3 grid(p.tiles_m * p.tiles_n);
+        std::vector<float> h0((size_t)m * n), h1((size_t)m * n);
+        for (int v = 0; v < NV; ++v) {  // every variant writes the same C (row stride aside)
+            if (sv[v].pad) continue;
+            GemmArgs q = pf; q.C = C;
+            CK(hipMemset(C, 0xff, (size_t)m * n * 4));
+            sv[v].fn<<<grid, 256>>>(q);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(v ? h1.data() : h0.data(), C, h0.size() * 4, hipMemcpyDeviceToHost));
+            if (v) printf("check %-14s %s\n", sv[v].name, memcmp(h0.data(), h1.data(), h0.size() * 4) ? "DIFF" : "same");
+        }
+        for (int r = 0; r < std::max(rounds, 3); ++r)
+            for (int v = 0; v < NV; ++v) {
+                GemmArgs q = pf; q.C = sv[v].pad ? Cp : C; q.csh = n + sv[v].pad;
+                for (int w = 0; w < 3; ++w) sv[v].fn<<<grid, 256>>>(q);
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < reps; ++i) sv[v].fn<<<grid, 256>>>(q);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                t[v].push_back(ms * 1000 / reps);
+            }
+        for (int v = 0; v < NV; ++v) {
+            std::sort(t[v].begin(), t[v].end());
+            printf("%-14s median %8.2f us  min %8.2f us\n", sv[v].name, t[v][t[v].size() / 2], t[v][0]);
+        }
+        return 0;
+    }
     if (only && std::string(only) == "clock") {
         struct SV { const char *name; KernelFn fn; int threads; unsigned long long *sym; };
         unsigned long long *pp_sym, *w4_sym;
