@@ -18,6 +18,15 @@ static void launch32(const float *X, int m, int k, PackedView vx, const float *W
     CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s, 32));
 }
 
+template <int kMap>
+static void launch32m(const float *X, int m, int k, PackedView vx, const float *W, int n, PackedView vw, hipStream_t s) {
+    const int nstrips = n / kW32Cols, npad = (int)((vw.rows_pad - n) / kW32Cols), nx = (int)(vx.rows_pad / 16);
+    pack_single_pass32_kernel<kMap><<<nstrips + npad + nx, 1024, 0, s>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad,
+                                                                          W, n, n, vw.scale, vw.q, vw.rows_pad, nstrips,
+                                                                          127.f, nullptr, 0);
+    CK(hipGetLastError());
+}
+
 int main(int argc, char **argv) {
     int m = argc > 1 ? atoi(argv[1]) : 2048, n = argc > 2 ? atoi(argv[2]) : 16384, k = argc > 3 ? atoi(argv[3]) : 4096;
     int reps = argc > 4 ? atoi(argv[4]) : 10;
@@ -50,7 +59,42 @@ int main(int argc, char **argv) {
     struct V { const char *name; std::function<void()> f; };
     std::vector<V> vs = {{"strip16", [&] { CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s0, n % 16 ? 8 : 16)); }},
                          {"strip8", [&] { CK(launch_pack_single_pass_kind(X, k, m, k, vx, W, n, n, vw, 127.f, s0, 8)); }},
-                         {"strip32", [&] { launch32(X, m, k, vx2, W, n, vw2, s0); }}};
+                         {"strip32", [&] { launch32(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"strip32 map1", [&] { launch32m<1>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"strip32 map2", [&] { launch32m<2>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"strip32 map3", [&] { launch32m<3>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c2 P4", [&] { launch32m<204>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c1 P8", [&] { launch32m<108>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c2 P2", [&] { launch32m<202>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c4 P4", [&] { launch32m<404>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c1 P16", [&] { launch32m<116>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c2 P8", [&] { launch32m<208>(X, m, k, vx2, W, n, vw2, s0); }},
+                         {"c8 P8", [&] { launch32m<808>(X, m, k, vx2, W, n, vw2, s0); }}};
+    for (int mp = 0; mp <= 4; ++mp) {  // every strip order writes the same bytes
+        CK(hipMemsetAsync(PW2, 0x5a, packed_bytes(n, k), s0));  // on s0: a non-blocking stream does not wait for the null stream
+        if (mp == 0) launch32m<0>(X, m, k, vx2, W, n, vw2, s0);
+        if (mp == 1) launch32m<1>(X, m, k, vx2, W, n, vw2, s0);
+        if (mp == 2) launch32m<2>(X, m, k, vx2, W, n, vw2, s0);
+        if (mp == 3) launch32m<3>(X, m, k, vx2, W, n, vw2, s0);
+        if (mp == 4) launch32m<204>(X, m, k, vx2, W, n, vw2, s0);
+        CK(hipStreamSynchronize(s0));
+        printf("map%d: ", mp); cmp(vw.q, vw2.q, vw.rows_pad * vw.k_pad, "w q");
+        printf("map%d: ", mp); cmp(vw.scale, vw2.scale, vw.rows_pad * 4, "w scale");
+        if (mp) {  // where the first differing byte is: (packed row, k) of the fragment-major layout
+            std::vector<int8_t> ha(vw.rows_pad * vw.k_pad), hb(ha.size());
+            CK(hipMemcpy(ha.data(), vw.q, ha.size(), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(hb.data(), vw2.q, hb.size(), hipMemcpyDeviceToHost));
+            int shown = 0;
+            for (int64_t r = 0; r < vw.rows_pad && shown < 4; ++r)
+                for (int64_t kk = 0; kk < vw.k_pad && shown < 4; ++kk)
+                    if (ha[fofs(r, kk, vw.k_pad)] != hb[fofs(r, kk, vw.k_pad)]) {
+                        printf("   row %lld k %lld: %d vs %d\n", (long long)r, (long long)kk, ha[fofs(r, kk, vw.k_pad)],
+                               hb[fofs(r, kk, vw.k_pad)]);
+                        ++shown;
+                        kk = vw.k_pad;  // next row
+                    }
+        }
+    }
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     std::vector<std::vector<float>> tm(vs.size());
     for (int r = 0; r < 5; ++r)

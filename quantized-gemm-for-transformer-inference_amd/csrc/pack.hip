@@ -847,6 +847,9 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
     }
 }
 
+// kMap (block -> strip order; lab A/B): 0 = XCD-contiguous strip ranges, 1 = strip = block, 2 = even strips
+// first then odd, 3 = strips 4j, then 4j + 1, ... (the blocks on the chip at one time spread over the row)
+template <int kMap = 0>
 __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
@@ -857,8 +860,28 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
     const int bid = blockIdx.x;
     const int npad = (int)((w_rows_pad - n) / kW32Cols);
     if (bid < nstrips) {
-        const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
-        const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        int strip;
+        if constexpr (kMap == 0) {
+            const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
+            strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+        } else if constexpr (kMap == 1) {
+            strip = bid;
+        } else if constexpr (kMap == 2) {
+            const int h = nstrips >> 1;
+            strip = (nstrips & 1) ? bid : (bid < h ? 2 * bid : 2 * (bid - h) + 1);
+        } else if constexpr (kMap == 3) {
+            const int q = nstrips >> 2;
+            strip = (nstrips & 3) ? bid : (bid % q) * 4 + bid / q;
+        } else {
+            // kMap = 100 c + P: P phases over groups of c adjacent strips; phase ph takes groups ph, ph + P, ...
+            constexpr int c = kMap / 100, P = kMap % 100;
+            if (nstrips % (c * P)) {
+                strip = bid;
+            } else {
+                const int per = nstrips / P, g = bid % c, j = (bid % per) / c, ph = bid / per;
+                strip = (j * P + ph) * c + g;
+            }
+        }
         pack_w_strip32_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kW32Cols;
@@ -1148,10 +1171,20 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
         const int nstrips = n / kW32Cols;
         const int npad = (int)((outw.rows_pad - n) / kW32Cols);
         const int nx = (int)(outx.rows_pad / 16);
-        pack_single_pass32_kernel<<<nstrips + npad + nx, 1024, 0, stream>>>(x, xsh, m, k, outx.scale, outx.q,
-                                                                            outx.rows_pad, outx.k_pad, w, wsh, n,
-                                                                            outw.scale, outw.q, outw.rows_pad, nstrips,
-                                                                            range, zero_words, nzero);
+        // strip order: groups of 2 adjacent strips, 4 phases (lab/pack32_lab.hip at 2048 x 16384 x 4096: 85.8-86.2
+        // vs 90.9-91.2 us for XCD-contiguous ranges; QGEMM_PACK32_ORDER=xcd restores those for A/B)
+        static const bool xcd_order = [] {
+            const char *e = getenv("QGEMM_PACK32_ORDER");
+            return e && e[0] == 'x';
+        }();
+        if (xcd_order)
+            pack_single_pass32_kernel<0><<<nstrips + npad + nx, 1024, 0, stream>>>(
+                x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
+                nstrips, range, zero_words, nzero);
+        else
+            pack_single_pass32_kernel<204><<<nstrips + npad + nx, 1024, 0, stream>>>(
+                x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
+                nstrips, range, zero_words, nzero);
         return hipGetLastError();
     }
     if (kind == 8) {
