@@ -70,7 +70,9 @@ int main(int argc, char **argv) {
                          {"c1 P16", [&] { launch32m<116>(X, m, k, vx2, W, n, vw2, s0); }},
                          {"c2 P8", [&] { launch32m<208>(X, m, k, vx2, W, n, vw2, s0); }},
                          {"c8 P8", [&] { launch32m<808>(X, m, k, vx2, W, n, vw2, s0); }}};
-    for (int mp = 0; mp <= 4; ++mp) {  // every strip order writes the same bytes
+    const bool only8 = n < 16384;  // the 32-column variants need n >= 16384 to mean anything
+    if (only8) vs = {vs[0], vs[1]};
+    for (int mp = 0; mp <= 4 && !only8; ++mp) {  // every strip order writes the same bytes
         CK(hipMemsetAsync(PW2, 0x5a, packed_bytes(n, k), s0));  // on s0: a non-blocking stream does not wait for the null stream
         if (mp == 0) launch32m<0>(X, m, k, vx2, W, n, vw2, s0);
         if (mp == 1) launch32m<1>(X, m, k, vx2, W, n, vw2, s0);
