@@ -204,6 +204,17 @@ def test_256_tile_kernel_ragged_shapes(qg, oracle, device, M, N, K):
     assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 1000, 5000), (257, 4104, 8193), (64, 520, 16384), (512, 2048, 12289)])
+def test_long_k_drop_in(qg, oracle, device, M, N, K):
+    """4096 < K <= 16384, row-major operands (the two-pass column pack of W and the fused X-row pass) -- ragged K,
+    the largest K, padding rows of the packed W (N not a multiple of 256), signed-seed quirk rows and columns;
+    every output bit."""
+    X, W = oracle.inputs(M, N, K, 151)
+    W[0, ::5] = -1.75  # those columns' signed seed (absmax quirk)
+    X[::7, 0] = -1.5
+    assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 4096, 2048), (1900, 4000, 3000), (1800, 4096, 4500)])
 def test_256_tile_split_k_plans(qg, oracle, device, M, N, K):
     """128 tiles of 256 x 256 with K >= 2048: the split-K plan (S = 2) on gemm_i8_fm -- slabs stored
