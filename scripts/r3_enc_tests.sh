@@ -1,0 +1,5 @@
+#!/bin/bash
+set -o pipefail
+out=gpurun_out/enc_tests; mkdir -p $out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_encoder.py > $out/pytest.log 2>&1 || { tail -30 $out/pytest.log; exit 1; }
+tail -1 $out/pytest.log

@@ -39,6 +39,26 @@ def test_add_layernorm_rows_bit_exact(qg, oracle, device, rows, w):
     assert_bits_equal(Y.cpu().numpy(), oracle.add_layernorm_rows(A, B), f"add+layernorm {rows}x{w}")
 
 
+@pytest.mark.parametrize("w", [1024, 1000, 4096, 260])
+def test_add_layernorm_rows_special_values(qg, oracle, device, w):
+    """The register-resident kernel's lane-hop sums (DPP wave_ror) on rows holding NaN, +-inf, -0, huge and tiny
+    values: the same rounding sequence as the column-order chain, bit for bit."""
+    rows = 12
+    A, B = oracle.uniform((rows, w), 21), oracle.uniform((rows, w), 22)
+    A[1, w // 3] = np.nan
+    A[2, 5] = np.inf
+    A[3, 7], B[3, 9] = np.inf, -np.inf
+    A[4, :] = -0.0
+    B[4, :] = -0.0
+    A[5, ::7] = 3.0e38
+    A[6, :] = 1e-40  # subnormal inputs
+    B[6, :] = 0.0
+    A[7, w - 1] = -2.5e9  # the last element of the row
+    A[8, 0] = 1e30  # the first
+    Y = qg.add_layernorm_rows(_dev(A, device), _dev(B, device))
+    assert_bits_equal(Y.cpu().numpy(), oracle.add_layernorm_rows(A, B), f"add+layernorm special values, w={w}")
+
+
 def test_add_layernorm_rows_misaligned_rows(qg, oracle, device):
     """Rows 4-byte aligned only (storage offset 1): the general kernel instead of the float4 one."""
     rows, w = 40, 1024
