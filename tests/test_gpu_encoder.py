@@ -111,6 +111,21 @@ def test_encoder_forward_bit_exact(qg, oracle, device, seq, d, H, dff, blocks):
         enc.close()
 
 
+@pytest.mark.parametrize("gain", [60.0, 1e4])
+def test_encoder_forward_peaked_softmax(qg, oracle, device, gain):
+    """Inputs scaled so the attention scores spread over hundreds to millions: most exps of a softmax row
+    underflow to +0 and the row sums (lane-hop chains in the fused attention) run over long runs of zeros and
+    a few large terms -- every output bit against the oracle."""
+    seq, d, H, dff, blocks = 100, 256, 8, 512, 2
+    X = oracle.uniform((seq, d), 29) * np.float32(gain)
+    enc = qg.Encoder(d, H, dff, blocks, max_seq=seq, seed=31)
+    try:
+        Y = enc.forward(_dev(X, device)).cpu().numpy()
+    finally:
+        enc.close()
+    assert_bits_equal(Y, oracle.encoder_forward(X, d, H, dff, blocks, 31), f"encoder, input x {gain}")
+
+
 def test_encoder_config5_bit_exact(qg, oracle, device):
     """BASELINE config 5: d_model 1024, seq 512 (16 heads, d_ff 4096, 2 blocks)."""
     seq, d, H, dff, blocks = 512, 1024, 16, 4096, 2
