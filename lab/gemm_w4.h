@@ -31,7 +31,7 @@ namespace gemm {
 
 enum W4Flags { kW4NoDma = 1, kW4NoRead = 2, kW4NoStore = 4, kW4Stamp = 8, kW4PadT = 16, kW4RowMajor = 32, kW4NoA = 64,
                kW4NoB = 128, kW4K1 = 256, kW4K4 = 512, kW4Sync = 1024,
-               kW4Nt = 2048, kW4NoPrio = 4096, kW4Direct = 8192, kW4Rot = 16384 };
+               kW4Nt = 2048, kW4NoPrio = 4096, kW4Direct = 8192, kW4Rot = 16384, kW4GScale = 32768 };
 
 #ifdef QGEMM_LAB
 __device__ unsigned long long g_w4_stamp[4096 * 6];
@@ -567,9 +567,14 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
         stamp(2);
         return;
     }
-    sCx[tid] = p.Cx[gi0 + tid];
-    sCw[tid] = p.Cw[gj0 + tid];
-    __syncthreads();
+    // kW4GScale: each wave reads the scales it needs straight from global memory (no LDS copy, no barrier: a
+    // wave whose k-loop ends first starts its epilogue at once)
+    constexpr bool kGS = (kFlags & kW4GScale) != 0;
+    if constexpr (!kGS) {
+        sCx[tid] = p.Cx[gi0 + tid];
+        sCw[tid] = p.Cw[gj0 + tid];
+        __syncthreads();
+    }
     float *T = reinterpret_cast<float *>(lds + wave * kBlockBytes);
     const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
                       gj0 + BN <= p.n;
@@ -578,9 +583,17 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
     const int r0 = wm * 128, c0 = wn * 128;
     // the scales into registers first: T and the scales share the one LDS array, so a scale read between
     // T stores would be re-issued (and waited for) after every store
-    float cwv[8];
+    float cwv[8], cxg[2][4][4];
 #pragma unroll
-    for (int ni = 0; ni < 8; ++ni) cwv[ni] = sCw[c0 + ni * 16 + lrow];
+    for (int ni = 0; ni < 8; ++ni) cwv[ni] = kGS ? p.Cw[gj0 + c0 + ni * 16 + lrow] : sCw[c0 + ni * 16 + lrow];
+    if constexpr (kGS) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int mq = 0; mq < 4; ++mq)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cxg[h][mq][r] = p.Cx[gi0 + r0 + 64 * h + mq * 16 + 4 * kq + r];
+    }
     if constexpr (kFlags & kW4Direct) {
         // ablation: dequantized straight from the accumulators, dword nontemporal stores (4 rows x 64 B per
         // wave instruction), no LDS image (full tiles only)
@@ -609,7 +622,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_i8_f4(GemmArgs p) {
 #pragma unroll
         for (int mq = 0; mq < 4; ++mq)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cxv[mq][r] = sCx[r0 + 64 * s + mq * 16 + 4 * kq + r];
+            for (int r = 0; r < 4; ++r) cxv[mq][r] = kGS ? cxg[s][mq][r] : sCx[r0 + 64 * s + mq * 16 + 4 * kq + r];
 #pragma unroll
         for (int ni = 0; ni < 8; ++ni) {
             const int jl = ni * 16 + lrow;

@@ -81,9 +81,10 @@ int main(int argc, char **argv) {
     if (only && std::string(only) == "stride") {
         float *Cp; CK(hipMalloc(&Cp, (size_t)m * (n + 64) * 4));
         struct SV { const char *name; KernelFn fn; int pad; };
-        constexpr int NV = 4;
+        constexpr int NV = 5;
         const SV sv[NV] = {{"f4nt", gemm_i8_f4<kW4Nt>, 0}, {"f4nt pad32", gemm_i8_f4<kW4Nt>, 32},
-                           {"f4nt pad64", gemm_i8_f4<kW4Nt>, 64}, {"f4nt rot", gemm_i8_f4<kW4Nt | kW4Rot>, 0}};
+                           {"f4nt pad64", gemm_i8_f4<kW4Nt>, 64}, {"f4nt rot", gemm_i8_f4<kW4Nt | kW4Rot>, 0},
+                           {"f4nt gscale", gemm_i8_f4<kW4Nt | kW4GScale>, 0}};
         hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
         std::vector<std::vector<float>> t(NV);
         dim3 grid(p.tiles_m * p.tiles_n);
