@@ -27,6 +27,15 @@ static void launch32m(const float *X, int m, int k, PackedView vx, const float *
     CK(hipGetLastError());
 }
 
+template <int kWpe>
+static void launch8w(const float *X, int m, int k, PackedView vx, const float *W, int n, PackedView vw, hipStream_t s) {
+    const int nstrips = n / kWs8Cols, npad = (int)((vw.rows_pad - n) / kWs8Cols), nx = (int)(vx.rows_pad / 8);
+    pack_single_pass8_kernel<kWpe><<<nstrips + npad + nx, 512, 0, s>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad,
+                                                                      W, n, n, vw.scale, vw.q, vw.rows_pad, nstrips,
+                                                                      127.f, nullptr, 0);
+    CK(hipGetLastError());
+}
+
 int main(int argc, char **argv) {
     int m = argc > 1 ? atoi(argv[1]) : 2048, n = argc > 2 ? atoi(argv[2]) : 16384, k = argc > 3 ? atoi(argv[3]) : 4096;
     int reps = argc > 4 ? atoi(argv[4]) : 10;
@@ -71,7 +80,20 @@ int main(int argc, char **argv) {
                          {"c2 P8", [&] { launch32m<208>(X, m, k, vx2, W, n, vw2, s0); }},
                          {"c8 P8", [&] { launch32m<808>(X, m, k, vx2, W, n, vw2, s0); }}};
     const bool only8 = n < 16384;  // the 32-column variants need n >= 16384 to mean anything
-    if (only8) vs = {vs[0], vs[1]};
+    if (only8) vs = {vs[0], vs[1], {"strip8 wpe4", [&] { launch8w<4>(X, m, k, vx2, W, n, vw2, s0); }},
+                     {"strip8 wpe6", [&] { launch8w<6>(X, m, k, vx2, W, n, vw2, s0); }},
+                     {"strip8 wpe8", [&] { launch8w<8>(X, m, k, vx2, W, n, vw2, s0); }}};
+    if (only8) {  // the waves-per-EU variants write the same bytes
+        for (int v = 4; v <= 8; v += 2) {
+            CK(hipMemsetAsync(PW2, 0x5a, packed_bytes(n, k), s0)); CK(hipMemsetAsync(PX2, 0x5a, packed_bytes(m, k), s0));
+            if (v == 4) launch8w<4>(X, m, k, vx2, W, n, vw2, s0);
+            if (v == 6) launch8w<6>(X, m, k, vx2, W, n, vw2, s0);
+            if (v == 8) launch8w<8>(X, m, k, vx2, W, n, vw2, s0);
+            CK(hipStreamSynchronize(s0));
+            printf("wpe%d: ", v); cmp(vw.q, vw2.q, vw.rows_pad * vw.k_pad, "w q");
+            printf("wpe%d: ", v); cmp(vx.q, vx2.q, vx.rows_pad * vx.k_pad, "x q");
+        }
+    }
     for (int mp = 0; mp <= 4 && !only8; ++mp) {  // every strip order writes the same bytes
         CK(hipMemsetAsync(PW2, 0x5a, packed_bytes(n, k), s0));  // on s0: a non-blocking stream does not wait for the null stream
         if (mp == 0) launch32m<0>(X, m, k, vx2, W, n, vw2, s0);

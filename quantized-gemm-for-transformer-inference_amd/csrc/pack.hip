@@ -1232,9 +1232,20 @@ hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, i
     const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
     const int nx = (int)(outx.rows_pad / 8);
     const OutlierMask om{bits, rank, count, xo, wo, wo_ld};
-    pack_single_pass8_kernel<5, true><<<nstrips + npad + nx, 512, 0, stream>>>(
-        x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad, nstrips,
-        range, nullptr, 0, om);
+    // a 4-waves-per-SIMD register budget (102 VGPRs, the same two blocks per CU): at 5 the masked body spilled
+    // 20 B per lane; QGEMM_MASKPACK_WPE=5 restores that build (A/B)
+    static const bool wpe5 = [] {
+        const char *e = getenv("QGEMM_MASKPACK_WPE");
+        return e && e[0] == '5';
+    }();
+    if (wpe5)
+        pack_single_pass8_kernel<5, true><<<nstrips + npad + nx, 512, 0, stream>>>(
+            x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
+            nstrips, range, nullptr, 0, om);
+    else
+        pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(
+            x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
+            nstrips, range, nullptr, 0, om);
     return hipGetLastError();
 }
 
