@@ -15,8 +15,10 @@ Extra objects on that line:
   roofline     -- the dominant kernel (the int8 GEMM): algorithmic 2*M*N*K int8 ops per launch over
                   its average launch time, measured with HIP events around each GEMM launch inside
                   the timed region, against the gfx950 dense int8 MFMA peak.
-  cpu_baseline -- the CPU oracle (a C restatement of the reference chain, oracle/) timed on a bounded
-                  row sample of the same workload on the host cores (rank 0, N=1 only).
+  cpu_baseline -- the CPU oracle (a C restatement of the reference chain, oracle/) timed on the host cores
+                  (rank 0, N=1 only): the FULL M=N=K=4096 problem repeated for ~--cpu-seconds (the oracle
+                  runs one whole chain in well under a second on 16 threads), plus the unquantized fp32
+                  op_mm restatement once on the full problem.
 """
 from __future__ import annotations
 
@@ -340,9 +342,6 @@ def c4_node(args, qg, dev, world, rank, distributed):
 def gemm_kernel_name(L, M, N, K, outlier):
     """The GEMM kernel this call launches, as the library plans it (qgemm_gemm_plan)."""
     if outlier:
-        if os.environ.get("QGEMM_OUTLIER_KERNEL", "").startswith("p"):
-            return ("gemm_i8_pp<2, kEpiOutlier> (256x256 tiles, 8 waves ping-pong, LDS-DMA ring, fused dequant + "
-                    "outlier fp32 chain on VALU)")
         return ("gemm_i8_fm<kEpiOutlier> (256x256 tiles, 4 waves of 128x128, fragment-major operands straight to "
                 "VGPRs, fused dequant + outlier fp32 chain on f32 MFMAs)")
     tile, name = ctypes.c_int(0), ctypes.c_char_p()

@@ -65,7 +65,11 @@ QGEMM_API int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_st
 /* ---- The chain's stages (the reference's L2 primitives, fused MI355X-style) ----------------
  * Packed operand = the quantized operand in MFMA-ready form, in ONE device buffer:
  *   [ scale: rows_pad f32 ][ reserved: parts x rows_pad u32, padded to 256 B ][ q: rows_pad x k_pad int8,
- *     row-major, zero padded ]   with parts = max(1, ceil((k-1)/256))
+ *     zero padded ]   with parts = max(1, ceil((k-1)/256))
+ * The q region is OPAQUE to callers: it is stored FRAGMENT-MAJOR (1-KiB blocks of 16 packed rows x 64 k,
+ * bytes in the lane order of one v_mfma_i32_16x16x64_i8 operand; csrc/qgemm_internal.h fofs), so the GEMM
+ * loads each MFMA operand with one contiguous 1-KiB load.  Treat a packed buffer as a handle: produce it
+ * with qgemm_pack_a / qgemm_pack_b, consume it with qgemm_mm_packed / qgemm_linear / the prepacked drop-in.
  * rows_pad = round_up(rows, 256), k_pad = round_up(k, 128).  For A, rows = m and the scale is
  * Cx (op_absmax(X,Cx), op_mm.cuh:76-77) and q = X_int8 (op_mm.cuh:86-87).  For B, rows = n
  * (B is stored transposed, k contiguous) and the scale is Cw (op_mm.cuh:78-79), q = W_int8^T.

@@ -60,6 +60,22 @@ QGEMM_API int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, 
  * in-place broadcast of [first[i], first[i] + count[i]) from rank root[i]. */
 QGEMM_API int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count, int *root, int max_ops);
 
+/* One planned collective of the one-process node path: on device index `rank`, root < 0 is an in-place
+ * ncclAllGather (send C + send_off, receive C + recv_off .. + ndev * count), root >= 0 an in-place
+ * ncclBroadcast of count floats at C + recv_off (= send_off) from rank `root`. */
+typedef struct qgemm_coll_op {
+    int rank;
+    int root;
+    int64_t send_off;
+    int64_t recv_off;
+    int64_t count;
+} qgemm_coll_op;
+
+/* The collectives qgemm_node_mm_quantize (mode 1 / 2) enqueues, as data (no GPU, no RCCL), in the order it
+ * issues them inside ONE ncclGroupStart/End: every rank's qgemm_allgather_plan operations, rank by rank.
+ * ops == NULL: returns the count; else fills up to max_ops and returns the count, or -hipErrorInvalidValue. */
+QGEMM_API int qgemm_node_allgather_plan(int m, int n, int ndev, qgemm_coll_op *ops, int max_ops);
+
 /* One process, ndev GPUs (the harness's -g): the whole-node C4 step.  mode 0: every device's shard
  * (op_mm_quantize_shard on devices[r] with A[r], B[r], C[r], streams[r]); mode 1: the shards, then the
  * all-gather of C over comms[r]; mode 2: the all-gather alone (timed separately by the harness). */

@@ -12,7 +12,7 @@
 
 #define QGEMM_LAB 1
 #include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
-#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
+#include "gemm_legacy.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;

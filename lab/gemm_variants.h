@@ -4,7 +4,7 @@
 
 #include <type_traits>
 
-#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
+#include "gemm_legacy.h"
 #include "gemm_sd.h"
 
 namespace qgemm {

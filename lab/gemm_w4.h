@@ -24,7 +24,7 @@
 // source swizzle as gemm_i8_pp (128-B rows, chunk g of row r in slot g ^ ((r>>1)&7)).
 #pragma once
 
-#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
+#include "gemm_legacy.h"
 
 namespace qgemm {
 namespace gemm {

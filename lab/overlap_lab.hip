@@ -13,7 +13,7 @@
 #include <hip/hip_ext.h>
 
 #include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
-#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
+#include "gemm_legacy.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;

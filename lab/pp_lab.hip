@@ -10,7 +10,7 @@
 #include <cstring>
 
 #define QGEMM_LAB 1
-#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
+#include "gemm_legacy.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;

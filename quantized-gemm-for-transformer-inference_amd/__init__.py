@@ -79,6 +79,7 @@ DIST_EXPORTED_SYMBOLS = (
     "qgemm_comm_destroy",
     "qgemm_allgather_rows",
     "qgemm_allgather_plan",
+    "qgemm_node_allgather_plan",
     "qgemm_node_mm_quantize",
 )
 COMM_ID_BYTES = 128
@@ -206,6 +207,8 @@ def load_dist() -> ctypes.CDLL:
         i64p = ctypes.POINTER(ctypes.c_int64)
         D.qgemm_allgather_plan.argtypes = [i32, i32, i32, i64p, i64p, ctypes.POINTER(i32), i32]
         D.qgemm_allgather_plan.restype = i32
+        D.qgemm_node_allgather_plan.argtypes = [i32, i32, i32, ctypes.POINTER(CollOp), i32]
+        D.qgemm_node_allgather_plan.restype = i32
         D.qgemm_node_mm_quantize.argtypes = [vp, vp, vp, i32, i32, i32, i32, ctypes.POINTER(i32), vp, vp, i32]
         D.qgemm_node_mm_quantize.restype = i32
         _dist = D
@@ -217,6 +220,26 @@ def shard_rows(m: int, world: int, rank: int) -> tuple:
     m0, rows = ctypes.c_int(), ctypes.c_int()
     _check("qgemm_shard_rows", load_dist().qgemm_shard_rows(m, world, rank, ctypes.byref(m0), ctypes.byref(rows)))
     return m0.value, rows.value
+
+
+class CollOp(ctypes.Structure):
+    """qgemm_coll_op (include/qgemm_dist.h): one planned collective of the one-process node path."""
+    _fields_ = [("rank", ctypes.c_int), ("root", ctypes.c_int), ("send_off", ctypes.c_int64),
+                ("recv_off", ctypes.c_int64), ("count", ctypes.c_int64)]
+
+
+def node_allgather_plan(m: int, n: int, ndev: int) -> list:
+    """The collectives qgemm_node_mm_quantize enqueues in its ONE RCCL group, in issue order, as
+    [(rank, root, send_off, recv_off, count)] (root -1: in-place all-gather; else an in-place broadcast)."""
+    D = load_dist()
+    cnt = D.qgemm_node_allgather_plan(m, n, ndev, None, 0)
+    if cnt < 0:
+        raise QGemmError("qgemm_node_allgather_plan", -cnt)
+    ops = (CollOp * max(1, cnt))()
+    got = D.qgemm_node_allgather_plan(m, n, ndev, ops, cnt)
+    if got != cnt:
+        raise QGemmError("qgemm_node_allgather_plan", -got if got < 0 else 1)
+    return [(o.rank, o.root, o.send_off, o.recv_off, o.count) for o in ops[:cnt]]
 
 
 def allgather_plan(m: int, n: int, world: int) -> list:
@@ -358,8 +381,9 @@ class Packed:
 
     @property
     def q(self):
-        """X_int8 (rows_pad x k_pad) or W_int8^T (n_pad x k_pad), zero padded, row-major (a copy, un-permuted
-        from the fragment-major storage: [rg][kb][kc][r][16 B] -> [rg][r][kb][kc][16 B])."""
+        """X_int8 (rows_pad x k_pad) or W_int8^T (n_pad x k_pad), zero padded, row-major -- a COPY, un-permuted
+        from the fragment-major storage ([rg][kb][kc][r][16 B] -> [rg][r][kb][kc][16 B]): writes into it do not
+        reach the packed buffer; in-place edits go through q_raw."""
         r16, kb = self.rows_pad // 16, self.k_pad // 64
         return (self.q_raw.view(r16, kb, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(self.rows_pad, self.k_pad))
 

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <vector>
+
 #include "../../include/qgemm_dist.h"
 
 namespace {
@@ -90,24 +92,63 @@ int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count
     return ops;
 }
 
+int qgemm_node_allgather_plan(int m, int n, int ndev, qgemm_coll_op *ops, int max_ops) {
+    if (m < 0 || n < 0 || ndev < 1 || max_ops < 0 || (max_ops > 0 && !ops)) return -(int)hipErrorInvalidValue;
+    // the per-rank plan is the same for every rank (it depends on m, n, world only); RCCL matches a
+    // communicator's collectives by their order inside the group, so every rank enqueues the list in plan order
+    std::vector<int64_t> first((size_t)ndev), count((size_t)ndev);
+    std::vector<int> root((size_t)ndev);
+    const int nplan = qgemm_allgather_plan(m, n, ndev, first.data(), count.data(), root.data(), ndev);
+    if (nplan < 0) return nplan;
+    const int64_t total = (int64_t)nplan * ndev;
+    if (ops == nullptr) return (int)total;  // size query
+    if (total > max_ops) return -(int)hipErrorInvalidValue;
+    int o = 0;
+    for (int r = 0; r < ndev; ++r)
+        for (int i = 0; i < nplan; ++i, ++o) {
+            qgemm_coll_op &op = ops[o];
+            op.rank = r;
+            op.root = root[i];
+            op.count = count[i];
+            op.recv_off = first[i];
+            // all-gather: rank r sends its own rows, in place inside the receive buffer; broadcast: the
+            // owner's rows, in place on every rank
+            op.send_off = root[i] < 0 ? first[i] + (int64_t)r * count[i] : first[i];
+        }
+    return o;
+}
+
+namespace {
+
+// enqueue one planned collective on its rank's communicator (inside the caller's group, if any)
+ncclResult_t issue(const qgemm_coll_op &op, float *C, ncclComm_t c, hipStream_t s) {
+    if (op.root < 0) return ncclAllGather(C + op.send_off, C + op.recv_off, (size_t)op.count, ncclFloat32, c, s);
+    return ncclBroadcast(C + op.send_off, C + op.recv_off, (size_t)op.count, ncclFloat32, op.root, c, s);
+}
+
+}  // namespace
+
 int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, void *comm, void *stream) {
     if (!C || !comm || m < 0 || n < 0 || world < 1 || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
     ncclComm_t c = static_cast<ncclComm_t>(comm);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    // the plan (qgemm_allgather_plan, tested on the CPU) executed on RCCL; at most world operations
-    constexpr int kMaxOps = 64;
-    int64_t first[kMaxOps], count[kMaxOps];
-    int root[kMaxOps];
-    if (world > kMaxOps) return (int)hipErrorInvalidValue;
-    const int ops = qgemm_allgather_plan(m, n, world, first, count, root, kMaxOps);
+    // the plan (qgemm_allgather_plan, tested on the CPU) executed on RCCL: at most world operations, sized
+    // from world (no fixed cap on the communicator size)
+    std::vector<int64_t> first((size_t)world), count((size_t)world);
+    std::vector<int> root((size_t)world);
+    const int ops = qgemm_allgather_plan(m, n, world, first.data(), count.data(), root.data(), world);
     if (ops < 0) return -ops;
     if (ops == 0) return 0;
-    if (ops == 1 && root[0] < 0)
-        return nccl_rc(ncclAllGather(C + (size_t)rank * (size_t)count[0], C + first[0], (size_t)count[0], ncclFloat32, c, s));
+    qgemm_coll_op op{};
+    op.rank = rank;
+    if (ops == 1 && root[0] < 0) {
+        op.root = -1, op.count = count[0], op.recv_off = first[0], op.send_off = first[0] + (int64_t)rank * count[0];
+        return nccl_rc(issue(op, C, c, s));
+    }
     ncclResult_t r = ncclGroupStart();
     for (int i = 0; i < ops && r == ncclSuccess; ++i) {
-        float *p = C + first[i];
-        r = ncclBroadcast(p, p, (size_t)count[i], ncclFloat32, root[i], c, s);
+        op.root = root[i], op.count = count[i], op.recv_off = first[i], op.send_off = first[i];
+        r = issue(op, C, c, s);
     }
     const ncclResult_t r2 = ncclGroupEnd();
     return nccl_rc(r != ncclSuccess ? r : r2);
@@ -126,14 +167,26 @@ int qgemm_node_mm_quantize(const float *const *A, const float *const *B, float *
         else rc = op_mm_quantize_shard(A[r], B[r], C[r], m, n, k, ndev, r, streams[r]);
     }
     if (rc == 0 && mode != 0 && ndev > 1) {
-        // one process drives every rank: the per-rank collectives go in one group
-        ncclResult_t g = ncclGroupStart();
-        for (int r = 0; r < ndev && rc == 0 && g == ncclSuccess; ++r) {
-            if ((he = hipSetDevice(devices[r])) != hipSuccess) rc = (int)he;
-            else rc = qgemm_allgather_rows(C[r], m, n, ndev, r, comms[r], streams[r]);
+        // one process drives every rank: ONE flat group holding every rank's planned collectives
+        // (qgemm_node_allgather_plan, checked on the CPU for every ndev and m % ndev), no nested groups
+        const int nops = qgemm_node_allgather_plan(m, n, ndev, nullptr, 0);
+        if (nops < 0) rc = -nops;
+        std::vector<qgemm_coll_op> ops(nops > 0 ? (size_t)nops : 0);
+        if (rc == 0 && nops > 0) {
+            const int got = qgemm_node_allgather_plan(m, n, ndev, ops.data(), nops);
+            if (got < 0) rc = -got;
         }
-        const ncclResult_t g2 = ncclGroupEnd();
-        if (rc == 0) rc = nccl_rc(g != ncclSuccess ? g : g2);
+        if (rc == 0 && nops > 0) {
+            ncclResult_t g = ncclGroupStart();
+            for (int i = 0; i < nops && rc == 0 && g == ncclSuccess; ++i) {
+                const qgemm_coll_op &op = ops[(size_t)i];
+                if ((he = hipSetDevice(devices[op.rank])) != hipSuccess) rc = (int)he;
+                else g = issue(op, C[op.rank], static_cast<ncclComm_t>(comms[op.rank]),
+                               static_cast<hipStream_t>(streams[op.rank]));
+            }
+            const ncclResult_t g2 = ncclGroupEnd();
+            if (rc == 0) rc = nccl_rc(g != ncclSuccess ? g : g2);
+        }
     }
     (void)hipSetDevice(prev);
     return rc;

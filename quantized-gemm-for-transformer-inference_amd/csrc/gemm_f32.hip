@@ -345,30 +345,6 @@ hipError_t launch_mm_f32_batched(const float *A, int64_t ash, int64_t asw, int64
     auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool fast = asw == 1 && ash % 4 == 0 && k % 4 == 0 && al16(A) && al16(B) && a_bs % 4 == 0 && b_bs % 4 == 0 &&
                       (bkc ? bsw % 4 == 0 : (bsw == 1 && bsh % 4 == 0 && n % 4 == 0)) && ash >= 0 && bsh >= 0 && bsw >= 0;
-    // lab knob (scripts/f32_probe.sh): QGEMM_F32_CFG=<n> forces one configuration
-    static const int forced = getenv("QGEMM_F32_CFG") ? atoi(getenv("QGEMM_F32_CFG")) : 0;
-    switch (forced) {
-        case 1: QG_F32(4, 4, 2, 2, 32); return hipGetLastError();
-        case 2: QG_F32(2, 2, 2, 2, 32); return hipGetLastError();
-        case 3: QG_F32(2, 2, 2, 2, 64); return hipGetLastError();
-        case 4: QG_F32(2, 2, 1, 1, 32); return hipGetLastError();
-        case 5: QG_F32(1, 2, 1, 1, 32); return hipGetLastError();
-        case 8: QG_F32(2, 2, 1, 1, 64); return hipGetLastError();
-        case 9: QG_F32(1, 2, 1, 1, 64); return hipGetLastError();
-        case 10: QG_F32(1, 1, 1, 1, 64); return hipGetLastError();
-        case 11: QG_F32(2, 2, 2, 2, 16); return hipGetLastError();
-        case 12: QG_F32(1, 2, 2, 2, 64); return hipGetLastError();
-        case 20: if (fast) { QG_DMA(2, 2, 2, 2, 32, 3); return hipGetLastError(); } break;
-        case 21: if (fast) { QG_DMA(1, 2, 1, 1, 32, 6); return hipGetLastError(); } break;
-        case 22: if (fast) { QG_DMA(1, 2, 1, 1, 32, 4); return hipGetLastError(); } break;
-        case 23: if (fast) { QG_DMA(2, 2, 1, 1, 32, 4); return hipGetLastError(); } break;
-        case 24: if (fast) { QG_DMA(1, 2, 2, 2, 32, 4); return hipGetLastError(); } break;
-        case 25: if (fast) { QG_DMA(4, 4, 2, 2, 32, 3); return hipGetLastError(); } break;
-        case 26: if (fast) { QG_DMA(2, 2, 2, 2, 32, 4); return hipGetLastError(); } break;
-        case 27: if (fast) { QG_DMA(1, 1, 1, 1, 32, 6); return hipGetLastError(); } break;
-        case 28: if (fast) { QG_DMA(1, 2, 2, 2, 32, 3); return hipGetLastError(); } break;
-        default: break;
-    }
     // the largest tile that still gives every SIMD two waves (4 x 256 CUs x 2); k is never split:
     // every output is one sequential chain
     auto waves = [&](int tm, int tn, int wpb) {

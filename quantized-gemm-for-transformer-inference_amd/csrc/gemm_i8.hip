@@ -7,8 +7,6 @@
 // by one kernel that reads the packed int8 operands once per macro-tile and writes fp32 O once.
 #include <hip/hip_ext.h>
 
-#include <cstdlib>
-
 #include "gemm_i8_kernels.h"
 
 namespace qgemm {
@@ -18,17 +16,6 @@ using namespace gemm;
 const char *gemm_config_name() { return "i8mfma16x16x64_t256x256_w4_wt128x128_fragmajor_direct_agpr"; }
 
 static thread_local GemmEvents t_events;
-// split-K 256-tile plans: 0 = gemm_i8_fm (product), 1 = the ping-pong kernel (QGEMM_SPLIT_KERNEL=pp: A/B)
-static const int g_split_kernel = [] {
-    const char *e = getenv("QGEMM_SPLIT_KERNEL");
-    return e && e[0] == 'p' ? 1 : 0;
-}();
-// the LLM.int8() outlier epilogue: 0 = gemm_i8_fm with the chain on f32 MFMAs (product), 1 = the ping-pong
-// kernel's VALU chain (QGEMM_OUTLIER_KERNEL=pp: A/B)
-static const int g_outlier_kernel = [] {
-    const char *e = getenv("QGEMM_OUTLIER_KERNEL");
-    return e && e[0] == 'p' ? 1 : 0;
-}();
 static int g_event_mode = 0;  // 0: hipExtLaunchKernel events, 1: hipEventRecord around the launch
 void set_gemm_event_mode(int mode) { g_event_mode = mode; }
 void set_gemm_events(hipEvent_t start, hipEvent_t stop) { t_events = GemmEvents{start, stop}; }
@@ -42,9 +29,9 @@ static bool shape_ok(const PackedView &a, const PackedView &b) {
     return a.k_pad == b.k_pad && a.rows_pad % BM == 0 && b.rows_pad % BN == 0 && a.k_pad % BK == 0;
 }
 
-// Launch plan.  256 x 256 tiles (gemm_i8_v3) while they give >= 128 blocks, with split-K below 160
+// Launch plan.  256 x 256 tiles (gemm_i8_fm) while they give >= 128 blocks, with split-K below 160
 // tiles when K is long: S = min(256 / tiles, k-steps / 8, 8) -- every slice keeps >= 8 k-steps
-// (scripts/split_probe.py: the slab round trip costs ~3-5 us).  Fewer 256-tiles: 64 x 64 tiles
+// (scripts/split_probe.py: the slab round trip costs ~3-5 us); 128 <= tiles < 160 makes S <= 2.  Fewer 256-tiles: 64 x 64 tiles
 // (gemm_i8_small<64>, four blocks per CU) with S = min(512 / tiles, k-steps / 16, 4) slices -- splits
 // only for K >= 4096.  Measured (gemm_lab small mode, us, 128-tiles vs 64-tiles at the chosen S):
 // 512x3072x1024 11.8 -> 7.6, 512x1024x1024 11.1 -> 6.1, 512x4096x1024 12.2 -> 8.1,
@@ -97,8 +84,6 @@ int gemm_plan_info(int m, int n, int k, int *tile, const char **kernel) {
         else if (g.tile == 64)
             *kernel = g.splits > 1 ? "gemm_i8_small<64> (64x64 tiles, LDS-DMA ring, split-K)"
                                    : "gemm_i8_small<64> (64x64 tiles, LDS-DMA ring)";
-        else if (g.splits > 1 && (g_split_kernel == 1 || g.splits != 2))
-            *kernel = "gemm_i8_pp<2> (256x256 tiles, 8 waves ping-pong, LDS-DMA ring, split-K)";
         else
             *kernel = g.splits > 1 ? "gemm_i8_fm<split-K> (256x256 tiles, 4 waves of 128x128, fragment-major operands "
                                      "straight to VGPRs, AGPR accumulators, int32 slabs + tickets)"
@@ -134,8 +119,9 @@ __global__ __launch_bounds__(256) void zero_tickets_kernel(unsigned *__restrict_
 }
 
 // 256 x 256 tiles: gemm_i8_fm (4 waves of 128 x 128, operands straight from the fragment-major packed
-// layout, no LDS in the main loop), split-K plans included; the ping-pong kernel (gemm_i8_pp<2>, on the same
-// layout) for the LLM.int8() outlier epilogue, which it implements.
+// layout, no LDS in the main loop) for every plan -- unsplit, 2-way split-K and the LLM.int8() outlier
+// epilogue.  (The ping-pong kernel gemm_i8_pp of round 2 is in lab/gemm_legacy.h: the 256-tile plan splits
+// in two or not at all, so no shape reached it without an environment switch)
 template <typename Launch>
 static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const GemmArgs &p, Launch kernel) {
     const GemmEvents ev = take_gemm_events();
@@ -152,12 +138,9 @@ static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const 
 
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
-    if (kEpi == kEpiOutlier && g_outlier_kernel == 1)  // QGEMM_OUTLIER_KERNEL=pp: the ping-pong kernel's VALU chain
-        return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF | kPPNtStore>);
-    if (p.splits > 1 && (g_split_kernel == 1 || p.splits != 2))
-        return launch_timed(grid, dim3(kThreads), stream, p, gemm_i8_pp<2, kEpi, kPPLayoutF | kPPNtStore>);
     if constexpr (kEpi != kEpiOutlier) {
-        if (p.splits > 1) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, true>);
+        if (p.splits == 2) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, true>);
+        if (p.splits > 2) return hipErrorNotSupported;  // gemm_plan never makes one (tiles in [128, 160) -> S <= 2)
     }
     return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);
 }

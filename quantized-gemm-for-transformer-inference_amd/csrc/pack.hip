@@ -18,6 +18,7 @@
 //   pack_rows_and_colmax : pack_rows(A) and pass 1 of pack_cols(B) in ONE launch (block roles), so
 //               the two HBM streams overlap and a launch boundary disappears.
 #include <algorithm>
+#include <atomic>
 
 #include "qgemm_internal.h"
 
@@ -1160,6 +1161,21 @@ hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, flo
 
 // kind: 0 = choose (the 8-column two-blocks-per-CU pass where it measured faster, else 16 columns),
 // 8 or 16 = force that strip width (lab)
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) of pack_single_pass_kernel, once per device
+static hipError_t pack16_lds_attr() {
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> set[kMaxDev];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    if (set[dev].load(std::memory_order_acquire)) return hipSuccess;
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(pack_single_pass_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 4 * kStageRowWordsMax);
+    if (e == hipSuccess) set[dev].store(1, std::memory_order_release);
+    return e;
+}
+
 hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
                                         int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind,
                                         uint32_t *zero_words, int nzero) {
@@ -1174,19 +1190,10 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
         const int npad = (int)((outw.rows_pad - n) / kW32Cols);
         const int nx = (int)(outx.rows_pad / 16);
         // strip order: groups of 2 adjacent strips, 4 phases (lab/pack32_lab.hip at 2048 x 16384 x 4096: 85.8-86.2
-        // vs 90.9-91.2 us for XCD-contiguous ranges; QGEMM_PACK32_ORDER=xcd restores those for A/B)
-        static const bool xcd_order = [] {
-            const char *e = getenv("QGEMM_PACK32_ORDER");
-            return e && e[0] == 'x';
-        }();
-        if (xcd_order)
-            pack_single_pass32_kernel<0><<<nstrips + npad + nx, 1024, 0, stream>>>(
-                x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
-                nstrips, range, zero_words, nzero);
-        else
-            pack_single_pass32_kernel<204><<<nstrips + npad + nx, 1024, 0, stream>>>(
-                x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
-                nstrips, range, zero_words, nzero);
+        // vs 90.9-91.2 us for XCD-contiguous ranges, the <0> instantiation the lab keeps)
+        pack_single_pass32_kernel<204><<<nstrips + npad + nx, 1024, 0, stream>>>(
+            x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
+            nstrips, range, zero_words, nzero);
         return hipGetLastError();
     }
     if (kind == 8) {
@@ -1206,10 +1213,12 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
     const int nx = (int)(outx.rows_pad / 16);
     // W strips: [16 waves][16 cols] partial maxima + 16 scales; X rows: 16 staged packed rows
     const size_t lds = std::max<size_t>(4096, (size_t)16 * 4 * (outx.k_pad / 4 + 16));
-    static const hipError_t lds_attr = hipFuncSetAttribute(reinterpret_cast<const void *>(pack_single_pass_kernel),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           16 * 4 * kStageRowWordsMax);
-    if (lds_attr != hipSuccess) return lds_attr;
+    // above 64 KiB of dynamic LDS (K > 4032) the kernel needs the attribute -- set once per DEVICE (one process may
+    // drive every GPU of a node, qgemm_node_mm_quantize); a failure is returned, not remembered
+    if (lds > 65536) {
+        const hipError_t lds_attr = pack16_lds_attr();
+        if (lds_attr != hipSuccess) return lds_attr;
+    }
     pack_single_pass_kernel<<<nstrips + npad + nx, 1024, lds, stream>>>(x, xsh, m, k, outx.scale, outx.q, outx.rows_pad,
                                                                          outx.k_pad, w, wsh, n, outw.scale, outw.q,
                                                                          outw.rows_pad, nstrips, range, zero_words,
@@ -1233,19 +1242,10 @@ hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, i
     const int nx = (int)(outx.rows_pad / 8);
     const OutlierMask om{bits, rank, count, xo, wo, wo_ld};
     // a 4-waves-per-SIMD register budget (102 VGPRs, the same two blocks per CU): at 5 the masked body spilled
-    // 20 B per lane; QGEMM_MASKPACK_WPE=5 restores that build (A/B)
-    static const bool wpe5 = [] {
-        const char *e = getenv("QGEMM_MASKPACK_WPE");
-        return e && e[0] == '5';
-    }();
-    if (wpe5)
-        pack_single_pass8_kernel<5, true><<<nstrips + npad + nx, 512, 0, stream>>>(
-            x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
-            nstrips, range, nullptr, 0, om);
-    else
-        pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(
-            x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
-            nstrips, range, nullptr, 0, om);
+    // 20 B per lane (profiles/r03_ab_maskpack_wpe.log)
+    pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(
+        x, xsh, m, k, outx.scale, outx.q, outx.rows_pad, outx.k_pad, w, wsh, n, outw.scale, outw.q, outw.rows_pad,
+        nstrips, range, nullptr, 0, om);
     return hipGetLastError();
 }
 

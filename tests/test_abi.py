@@ -184,3 +184,77 @@ def test_allgather_plan_reassembles_every_rank(qg, world):
     D = qg.load_dist()
     assert D.qgemm_allgather_plan(-1, 4, 2, None, None, None, 0) < 0
     assert D.qgemm_allgather_plan(8, 4, 2, None, None, None, 0) < 0  # one op needed, no room
+
+
+def _simulate_node_group(ops, m, n, ndev, qg):
+    """Run one RCCL group of planned collectives the way RCCL matches them: the i-th collective on every
+    communicator forms one operation, so every rank must list the same (kind, root, count, recv_off) sequence;
+    then execute them on per-rank numpy buffers that start with only the rank's own shard."""
+    import numpy as np
+    per = [[o for o in ops if o[0] == r] for r in range(ndev)]
+    assert all(len(p) == len(per[0]) for p in per), "every communicator enqueues the same number of ops"
+    full = np.arange(m * n, dtype=np.float64) + 1
+    bufs = []
+    for r in range(ndev):
+        b = np.zeros(m * n)
+        m0, rows = qg.shard_rows(m, ndev, r)
+        b[m0 * n:(m0 + rows) * n] = full[m0 * n:(m0 + rows) * n]
+        bufs.append(b)
+    for i in range(len(per[0])):
+        col = [per[r][i] for r in range(ndev)]
+        keys = {(root, count, recv) for (_, root, _, recv, count) in col}
+        assert len(keys) == 1, f"op {i}: ranks disagree on the collective {col}"
+        root, count, recv = keys.pop()
+        if root < 0:  # all-gather: rank r contributes [send_off, send_off + count), which must be its own rows
+            sent = []
+            for (r, _, send, _, _) in col:
+                m0, rows = qg.shard_rows(m, ndev, r)
+                assert send == recv + r * count and send == m0 * n and count == rows * n, "in-place send = own rows"
+                sent.append(bufs[r][send:send + count].copy())
+            for b in bufs:
+                for r in range(ndev):
+                    b[recv + r * count:recv + (r + 1) * count] = sent[r]
+        else:  # broadcast from root, in place: the root's own rows
+            m0, rows = qg.shard_rows(m, ndev, root)
+            assert recv == m0 * n and count == rows * n, "a broadcast moves exactly its root's rows"
+            assert all(send == recv for (_, _, send, _, _) in col), "in place"
+            src = bufs[root][recv:recv + count].copy()
+            for b in bufs:
+                b[recv:recv + count] = src
+    return full, bufs
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 4, 5, 7, 8])
+def test_node_allgather_plan_assembles_every_device(qg, ndev):
+    """The one-process node path (qgemm_node_mm_quantize mode 1 / 2, the harness's -g) issues exactly
+    qgemm_node_allgather_plan's list inside ONE flat RCCL group (no GPU needed to check its
+    argument and group logic).  For equal shards (m % ndev == 0) and unequal ones, including m < ndev: every
+    communicator lists the same collectives in the same order, every send is the rank's own rows, and running
+    them assembles the whole C on every device."""
+    import numpy as np
+    for m in (1, 3, 8, 24, 65, 96, 1001, 65536 + 3):
+        n = 3
+        ops = qg.node_allgather_plan(m, n, ndev)
+        plan = qg.allgather_plan(m, n, ndev)
+        assert len(ops) == ndev * len(plan)
+        assert [o[0] for o in ops] == sorted(o[0] for o in ops), "rank by rank, in plan order"
+        if m % ndev == 0:
+            assert len(plan) == 1 and plan[0][2] == -1
+        else:
+            assert all(root >= 0 for _, _, root in plan) and len(plan) == min(m, ndev)
+        full, bufs = _simulate_node_group(ops, m, n, ndev, qg)
+        for r, b in enumerate(bufs):
+            assert np.array_equal(b, full), f"m={m} ndev={ndev} device {r}"
+    assert qg.node_allgather_plan(0, 4, ndev) == [] and qg.node_allgather_plan(8, 0, ndev) == []
+    D = qg.load_dist()
+    assert D.qgemm_node_allgather_plan(-1, 4, ndev, None, 0) < 0
+    assert D.qgemm_node_allgather_plan(5, 4, ndev, (qg.CollOp * 1)(), 1) < 0  # ndev ops needed, room for one
+
+
+def test_allgather_plan_has_no_world_cap(qg):
+    """qgemm_allgather_rows sizes its plan from the world size (a fixed 64-op cap refused
+    communicators above 64 ranks even for the one-all-gather plan)."""
+    assert qg.allgather_plan(128 * 4, 2, 128) == [(0, 8, -1)]
+    assert len(qg.allgather_plan(129, 2, 128)) == 128
+    D = qg.load_dist()
+    assert D.qgemm_allgather_rows(None, 512, 2, 128, 0, None, None) == 1  # still the argument check, not a cap

@@ -64,12 +64,13 @@ def test_outlier_fast_path_nan_and_none(qg, oracle, device):
     assert_bits_equal(C.cpu().numpy(), want, "fast path, NaN column")
 
 
-@pytest.mark.parametrize("ncols", [1, 3])
+@pytest.mark.parametrize("ncols", [0, 1, 3])
 def test_outlier_chain_keeps_negative_zero(qg, oracle, device, ncols):
     """An outlier chain that underflows to -0 added to an int8 part that is -0: O = fl(-0 + -0) = -0.  The GEMM
     epilogue runs the chain on 4-column f32 MFMA steps, so a count that is not a multiple of 4 pads the last
     step -- with +0 * -0, which leaves a -0 sum alone (+0 * +0 would give +0).  O8[5, 11] is -0: acc < 0 times
-    an outer product Cx * Cw that underflows to +0."""
+    an outer product Cx * Cw that underflows to +0.  ncols = 0: no column crosses the threshold, so the fast
+    path's epilogue must store O8 with no add (fl(-0 + +0) would be +0)."""
     M, N, K = 2560, 4096, 128  # the fast path: 160 256-tiles
     X, W = oracle.inputs(M, N, K, 12)
     cols = [7, 40, 90][:ncols]
@@ -86,6 +87,8 @@ def test_outlier_chain_keeps_negative_zero(qg, oracle, device, ncols):
     assert cnt == wcnt == ncols
     assert want[5, 11] == 0.0 and np.signbit(want[5, 11]), "the oracle's value is -0"
     assert_bits_equal(C.cpu().numpy(), want, f"outlier chain -0, {ncols} columns")
+    if ncols == 0:
+        assert_bits_equal(want, oracle.quantized_mm(X, W), "zero outlier columns = the plain path")
 
 
 def test_no_outliers_is_the_plain_path(qg, oracle, device):

@@ -517,12 +517,12 @@ def test_lds_dma_rings_repeat_race_screen(qg, oracle, device):
 
 
 @pytest.mark.parametrize("K", [128, 256, 384, 640])
-def test_pingpong_ring_l2_hot_repeat(qg, oracle, device, K):
-    """Race screen of the 256-tile ping-pong GEMM's LDS ring with the DMA source hot in L2: 256 tiles
-    (no split-K), one to five k-steps, so every panel is tiny and re-read by the XCD's other tiles and
-    the LDS-DMA lands as fast as it can; 20 back-to-back calls, every output bit.  (Staging mode 1 let
-    a lead wave's DMA overwrite A rows a lag wave was still reading: wrong whenever the DMA beats
-    ~28 MFMAs -- ADVICE r2.)"""
+def test_fm_short_k_l2_hot_repeat(qg, oracle, device, K):
+    """gemm_i8_fm (the 256-tile kernel, no split-K) at one to five 128-deep k-steps: every operand panel is tiny
+    and re-read by the XCD's other tiles, so the fragment loads land as fast as they can and the epilogue's
+    per-wave LDS blocks are reused right behind the k-loop; the three register sets' clamped loads past the
+    last sub-step are exercised at every remainder (K / 64 = 2, 4, 6, 10); 20 back-to-back calls, every output
+    bit.  (Round 2 screened the ping-pong kernel's LDS ring here; that kernel is lab-only since round 4.)"""
     M = N = 4096
     X, W = oracle.inputs(M, N, K, 131)
     want = oracle.quantized_mm(X, W)
