@@ -1,7 +1,7 @@
 // t2_lab.hip -- LAB harness for gemm_t2.h (two teams of 4 waves per 256 x 256 tile) against the product
 // gemm_i8_fm, bit-checked, timed in interleaved rounds in one process; `clock` mode: in-kernel stamps per team.
 //   build/t2_lab m n k rounds spec[,spec...] [clock]
-// spec: fm | t2 | t2ns | t2nl | t2np | t2late | t2s:N (team 1 sleeps N x 512 cycles) | t2p:N (team 0 at
+// spec: fm | fms (fm split-K 2) | fk (in-CU split-K, 256 x 128 regions) | t2 | t2ns | t2nl | t2np | t2late | t2s:N (team 1 sleeps N x 512 cycles) | t2p:N (team 0 at
 //       priority 2 for its first N sub-steps) | t2sp:N:M (both)
 #include <cstdio>
 #include <cstdlib>
@@ -36,12 +36,15 @@ struct Variant {
     bool stamped;    // a stamping build exists
     KernelFn sfn;    // the stamping build
     bool nostore;
+    int kind = 0;    // 0: 256-tile grid, 1: fm split-K 2 (slabs + tickets), 2: fk (256 x 128 regions)
 };
 
 static Variant make(const std::string &spec) {
     Variant v{spec, nullptr, 512, 0, 0, true, nullptr, false};
     int a = 0, b = 0;
     if (spec == "fm") { v.fn = gemm_i8_fm<>; v.threads = 256; v.stamped = false; }
+    else if (spec == "fms") { v.fn = gemm_i8_fm<kEpiNone, false, true>; v.threads = 256; v.stamped = false; v.kind = 1; }
+    else if (spec == "fk") { v.fn = gemm_i8_fk<>; v.threads = 256; v.stamped = false; v.kind = 2; }
     else if (spec == "t2") { v.fn = gemm_i8_t2<kT2Nt>; v.sfn = gemm_i8_t2<kT2Nt | kT2Stamp>; }
     else if (spec == "t2plain") { v.fn = gemm_i8_t2<0>; v.sfn = gemm_i8_t2<kT2Stamp>; }
     else if (spec == "t2ns") { v.fn = gemm_i8_t2<kT2NoStore>; v.sfn = gemm_i8_t2<kT2NoStore | kT2Stamp>; v.nostore = true; }
@@ -89,6 +92,16 @@ int main(int argc, char **argv) {
     p.tiles_m = m / BM; p.tiles_n = n / BN; p.inv_r2 = 1.0f / (127.0f * 127.0f); p.splits = 1;
     const int nb = p.tiles_m * p.tiles_n;
     dim3 grid(nb);
+    int32_t *slabs; unsigned *tickets;
+    CK(hipMalloc(&slabs, (size_t)nb * 2 * 256 * 256 * 4)); CK(hipMalloc(&tickets, 4096 * 4));
+    CK(hipMemset(tickets, 0, 4096 * 4));
+    auto args = [&](const Variant &v) {
+        GemmArgs q = p;
+        if (v.kind == 1) { q.splits = 2; q.slabs = slabs; q.tickets = tickets; q.reset_tickets = 1; }
+        if (v.kind == 2) q.tiles_n = n / 128;
+        return q;
+    };
+    auto grid_of = [&](const Variant &v) { return dim3(v.kind ? nb * 2 : nb); };
 
     if (clock) {
         unsigned long long *sym;
@@ -141,7 +154,7 @@ int main(int argc, char **argv) {
         set_params(v);
         for (int rep = 0; rep < 2; ++rep) {
             CK(hipMemset(C, 0xff, (size_t)m * n * 4));
-            v.fn<<<grid, v.threads>>>(p);
+            v.fn<<<grid_of(v), v.threads>>>(args(v));
             CK(hipDeviceSynchronize());
             CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
             size_t bad = 0;
@@ -156,9 +169,11 @@ int main(int argc, char **argv) {
     for (int r = 0; r < rounds; ++r)
         for (size_t vi = 0; vi < vs.size(); ++vi) {
             set_params(vs[vi]);
-            for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, vs[vi].threads>>>(p);
+            const GemmArgs pa = args(vs[vi]);
+            const dim3 g = grid_of(vs[vi]);
+            for (int w = 0; w < 3; ++w) vs[vi].fn<<<g, vs[vi].threads>>>(pa);
             CK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, vs[vi].threads>>>(p);
+            for (int i = 0; i < reps; ++i) vs[vi].fn<<<g, vs[vi].threads>>>(pa);
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             t[vi].push_back(ms * 1000 / reps);

@@ -459,24 +459,28 @@ __global__ __launch_bounds__(256) void colmax_kernel(const float *__restrict__ s
 }
 
 // Fused: blocks [0, ncol) run pass 1 of pack_cols(B), blocks [ncol, ncol + nrow) run pack_rows(A).
-template <int R>
+// kXFirst: the X-row blocks come first in dispatch order and W's column-max sweep last, so W's rows are the most
+// recent bytes in the Infinity Cache when pass 2 starts (it re-reads them in reverse: pack_cols_kernel<.., true>)
+template <int R, bool kXFirst = false>
 __global__ __launch_bounds__(256) void pack_rows_and_colmax_kernel(
     const float *__restrict__ a, int64_t ash, int m, int k, float *__restrict__ a_scale, int8_t *__restrict__ a_q,
     int64_t a_rows_pad, int64_t k_pad, const float *__restrict__ b, int64_t bsh, int n,
     uint32_t *__restrict__ b_partial, int64_t b_rows_pad, int col_blocks, int ncol, float range, uint32_t *zero_words,
     int nzero) {
     __shared__ float red[4 * 256];
-    const int bid = blockIdx.x;
+    const int nrow = (int)gridDim.x - ncol;
+    // role index: column-max blocks [0, ncol), X-row blocks [ncol, ncol + nrow) (rotated when kXFirst)
+    const int bid = kXFirst ? ((int)blockIdx.x < nrow ? (int)blockIdx.x + ncol : (int)blockIdx.x - nrow) : (int)blockIdx.x;
     zero_words_block0(zero_words, nzero);
     if (bid < ncol) {
         // unrolled 4 deep: pack3_lab `call_u4` 140.9-146.0 vs 143.6-149.4 us for 8 (FFN down, pass 1 + pass 2)
         colmax_body<true, 4>(bid % col_blocks, bid / col_blocks, b, bsh, k, n, b_partial, b_rows_pad, red);
     } else if constexpr (R < 0) {
-        pack_row_block_body(xcd_contig(bid, ncol, gridDim.x - ncol), a, ash, m, k, range, a_scale, a_q, a_rows_pad, k_pad,
-                            red);
+        pack_row_block_body(kXFirst ? xcd_contig(blockIdx.x, 0, nrow) : xcd_contig(bid, ncol, nrow), a, ash, m, k, range,
+                            a_scale, a_q, a_rows_pad, k_pad, red);
     } else {
-        pack_rows_vec_body<R>(xcd_contig(bid, ncol, gridDim.x - ncol), a, ash, m, k, range, a_scale, a_q, a_rows_pad,
-                              k_pad);
+        pack_rows_vec_body<R>(kXFirst ? xcd_contig(blockIdx.x, 0, nrow) : xcd_contig(bid, ncol, nrow), a, ash, m, k, range,
+                              a_scale, a_q, a_rows_pad, k_pad);
     }
 }
 
@@ -516,7 +520,9 @@ __device__ __forceinline__ void load_col_tile(float4 (&x)[2][4], const float *__
 // (FFN down W): 2 / 4 / 8 / 16 / 32 tiles per block 70.1 / 74.7 / 69.2 / 68.9 / 87.8 us.
 constexpr int kTilesPerBlock = 8;
 
-template <bool VEC, int kTPB = kTilesPerBlock>
+// kRev: the k-ranges in reverse dispatch order (bottom rows of W first): pass 1 swept W top to bottom, so its
+// last rows are the ones still in the Infinity Cache
+template <bool VEC, int kTPB = kTilesPerBlock, bool kRev = false>
 __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
                                                         float range, const uint32_t *__restrict__ partial,
                                                         int64_t parts, int64_t rows_pad, float *__restrict__ scale,
@@ -526,7 +532,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
     const int t = threadIdx.x;
     const int64_t n0 = (int64_t)blockIdx.x * kTc;
     const int64_t nkt = k_pad / kTk;
-    const int64_t kt0 = (int64_t)blockIdx.y * kTPB;
+    const int by = kRev ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
+    const int64_t kt0 = (int64_t)by * kTPB;
     const int64_t kt1 = min(nkt, kt0 + kTPB);
     const int col4 = t & 15;  // 4 input columns n0 + 4*col4 .. +3
     const int rg = t >> 4;    // rows k0 + 4*rg + 64*h + {0..3}
@@ -545,7 +552,7 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
             s = inv_divide(range, cx);
         }
         s_sh[t] = s;
-        if (blockIdx.y == 0) scale[j] = cx;
+        if (by == 0) scale[j] = cx;
     }
     __syncthreads();
     const float s0 = s_sh[4 * col4 + 0], s1 = s_sh[4 * col4 + 1], s2 = s_sh[4 * col4 + 2], s3 = s_sh[4 * col4 + 3];
