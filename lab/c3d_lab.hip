@@ -14,7 +14,7 @@
 #include <cstring>
 
 #include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
-#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8_kernels.h"
+#include "gemm_fk.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;

@@ -12,6 +12,7 @@
 
 #define QGEMM_LAB 1
 #include "gemm_t2.h"
+#include "gemm_fk.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;

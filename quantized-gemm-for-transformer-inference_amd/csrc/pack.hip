@@ -839,7 +839,19 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
         if (r0 >= k_pad) continue;
         float4 x4[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x4[e] = i < kW32RegI ? v[i < kW32RegI ? i : 0][e] : ls[((i - kW32RegI) * 4 + e) * 16 * 64];
+        for (int e = 0; e < 4; ++e) {
+            if (i < kW32RegI) {
+                x4[e] = v[i < kW32RegI ? i : 0][e];
+            } else {
+                // one ds_read_b128 per slot (volatile: hipcc had split the first of these reads into
+                // ds_read2_b32 + 2 ds_read_b32, whose lane-linear 16-B stride is a 4-way bank conflict per
+                // dword -- all of this pack's LDS bank-conflict cycles, lab/ldsattr_lab.hip)
+                typedef float v4f_t __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(3))) const volatile v4f_t lds_v4f_t;
+                const v4f_t y = *(lds_v4f_t *)(ls + ((i - kW32RegI) * 4 + e) * 16 * 64);
+                x4[e] = make_float4(y.x, y.y, y.z, y.w);
+            }
+        }
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
             int qe[4];
@@ -1145,12 +1157,16 @@ hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int col
                                   hipStream_t stream) {
     const dim3 g2((unsigned)(out.rows_pad / kTc), (unsigned)((out.k_pad / kTk + kTilesPerBlock - 1) / kTilesPerBlock));
     const int64_t parts = len > 1 ? out.parts : 0;  // K = 1: no candidates, Cw = seed
+    // bottom rows of W first: pass 1 swept W top to bottom, so its last rows are still in the Infinity Cache
+    // (lab/c3d_lab.hip, FFN down: pass 2 72.5 -> 64.2 us with X-first pass 1, profiles/r04_c3d_order_lab.log)
     if (cols_vec_ok(src, sh, cols))
-        pack_cols_kernel<true><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch, parts, out.rows_pad,
-                                                       out.scale, out.q, out.k_pad);
+        pack_cols_kernel<true, kTilesPerBlock, true><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch,
+                                                                             parts, out.rows_pad, out.scale, out.q,
+                                                                             out.k_pad);
     else
-        pack_cols_kernel<false><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch, parts, out.rows_pad,
-                                                        out.scale, out.q, out.k_pad);
+        pack_cols_kernel<false, kTilesPerBlock, true><<<g2, 256, 0, stream>>>(src, sh, len, cols, range, out.scratch,
+                                                                              parts, out.rows_pad, out.scale, out.q,
+                                                                              out.k_pad);
     return hipGetLastError();
 }
 
@@ -1278,8 +1294,10 @@ hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k
     const int ncol = col_blocks * (int)outb.parts;
     const int rr = rows_regs(k);
     const int nrow = (int)(rr < 0 ? outa.rows_pad : outa.rows_pad / 4);  // block per row / 4 rows per block
+    // X's row blocks first, W's column-max sweep last: W's rows are then the most recent bytes in the Infinity Cache
+    // when pass 2 re-reads them bottom-up (lab/c3d_lab.hip, FFN down, one box, interleaved: call 291.1 -> 282.9 us)
 #define QG_FUSED(Rv)                                                                                            \
-    pack_rows_and_colmax_kernel<Rv><<<ncol + nrow, 256, 0, stream>>>(a, ash, m, k, outa.scale, outa.q,          \
+    pack_rows_and_colmax_kernel<Rv, true><<<ncol + nrow, 256, 0, stream>>>(a, ash, m, k, outa.scale, outa.q,          \
                                                                      outa.rows_pad, outa.k_pad, b, bsh, n,       \
                                                                      outb.scratch, outb.rows_pad, col_blocks,    \
                                                                      ncol, range, zero_words, nzero)
