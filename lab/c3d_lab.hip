@@ -4,7 +4,8 @@
 //   P1 W-first (library) | X-first (W's column-max sweep last: W's bottom rows are the most recent bytes in the
 //      Infinity Cache when pass 2 starts)
 //   P2 fwd (library, top rows first) | rev (bottom rows first: re-reads what pass 1 read last)
-//   G  fms (gemm_i8_fm split-K 2: slabs + tickets, library) | fk (gemm_i8_fk: split-K inside the CU)
+//   G  gemm_i8_fm split-K 2 with both slabs (rounds 2-3) | ticket-first (one slab, uneven K split: round 4) |
+//      fk (gemm_i8_fk: split-K inside the CU)
 //   build/c3d_lab m n k rounds
 #include <cstdio>
 #include <cstdlib>
@@ -57,34 +58,38 @@ int main(int argc, char **argv) {
             pack_cols_kernel<true, kTilesPerBlock, false><<<g2, 256, 0, s0>>>(W, n, k, n, range, vw.scratch, vw.parts,
                                                                               vw.rows_pad, vw.scale, vw.q, vw.k_pad);
     };
-    auto gemm = [&](bool fk, float *out) {
+    // g: 0 = fm split-K both slabs (rounds 2-3), 1 / 2 = ticket-first split-K with slice 0 = 30 / 31 of 64 k-steps,
+    // 3 = fk (split-K inside the CU), 4 = ticket-first 31 with the XCD-pair map
+    auto gemm = [&](int g, float *out) {
         GemmArgs p{};
         p.A = vx.q; p.B = vw.q; p.Cx = vx.scale; p.Cw = vw.scale; p.C = out; p.csh = n; p.csw = 1; p.m = m; p.n = n;
         p.k_pad = vx.k_pad; p.tiles_m = tiles_m; p.inv_r2 = 1.0f / (range * range); p.splits = 1;
-        if (fk) {
+        if (g == 3) {
             p.tiles_n = n / 128;
             gemm_i8_fk<><<<tiles * 2, 256, 0, s0>>>(p);
-        } else {
-            p.tiles_n = tiles_n; p.splits = 2; p.slabs = slabs; p.tickets = tickets; p.reset_tickets = 1;
-            gemm_i8_fm<kEpiNone, false, true><<<tiles * 2, 256, 0, s0>>>(p);
+            return;
         }
+        p.tiles_n = tiles_n; p.splits = 2; p.slabs = slabs; p.tickets = tickets; p.reset_tickets = 1;
+        if (g == 0) gemm_i8_fm<kEpiNone, false, kSplitBoth><<<tiles * 2, 256, 0, s0>>>(p);
+        if (g == 1) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 30><<<tiles * 2, 256, 0, s0>>>(p);
+        if (g == 2) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31><<<tiles * 2, 256, 0, s0>>>(p);
+        if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);
     };
-    struct V { std::string name; bool xf, rev, fk; };
+    struct V { std::string name; bool xf, rev; int g; };
     std::vector<V> vs;
-    for (int g = 0; g < 2; ++g)
+    const char *gn[5] = {"_both", "_first30", "_first31", "_fk", "_first31pair"};
+    for (int g : {0, 2, 4})
         for (int a = 0; a < 2; ++a)
-            for (int b = 0; b < 2; ++b)
-                vs.push_back({std::string(a ? "xfirst" : "wfirst") + (b ? "_rev" : "_fwd") + (g ? "_fk" : "_fms"), a != 0,
-                              b != 0, g != 0});
+            vs.push_back({std::string(a ? "xfirst_rev" : "wfirst_fwd") + gn[g], a != 0, a != 0, g});
     // reference: the library's order
-    pass1(false); pass2(false); gemm(false, Cref);
+    pass1(false); pass2(false); gemm(0, Cref);
     CK(hipStreamSynchronize(s0));
     std::vector<float> href((size_t)m * n), hgot(href.size());
     CK(hipMemcpy(href.data(), Cref, href.size() * 4, hipMemcpyDeviceToHost));
     for (auto &v : vs) {
         CK(hipMemsetAsync(C, 0xff, (size_t)m * n * 4, s0));
         CK(hipMemsetAsync(vw.q, 0x5a, vw.rows_pad * vw.k_pad, s0));
-        pass1(v.xf); pass2(v.rev); gemm(v.fk, C);
+        pass1(v.xf); pass2(v.rev); gemm(v.g, C);
         CK(hipStreamSynchronize(s0));
         CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
         printf("check %-18s %s\n", v.name.c_str(), memcmp(href.data(), hgot.data(), href.size() * 4) ? "DIFF" : "same");
@@ -93,16 +98,16 @@ int main(int argc, char **argv) {
     hipEvent_t ev[4];
     for (auto &e : ev) CK(hipEventCreate(&e));
     std::vector<std::vector<float>> tc(vs.size()), t1(vs.size()), t2(vs.size()), tg(vs.size());
-    for (int i = 0; i < 300; ++i) { pass1(false); pass2(false); gemm(false, C); }  // clocks up
+    for (int i = 0; i < 300; ++i) { pass1(false); pass2(false); gemm(0, C); }  // clocks up
     for (int r = 0; r < rounds; ++r)
         for (size_t i = 0; i < vs.size(); ++i) {
             const V &v = vs[i];
-            for (int w = 0; w < 3; ++w) { pass1(v.xf); pass2(v.rev); gemm(v.fk, C); }
+            for (int w = 0; w < 3; ++w) { pass1(v.xf); pass2(v.rev); gemm(v.g, C); }
             float a1 = 0, a2 = 0, ag = 0, ac = 0;
             for (int j = 0; j < reps; ++j) {
                 CK(hipEventRecord(ev[0], s0)); pass1(v.xf);
                 CK(hipEventRecord(ev[1], s0)); pass2(v.rev);
-                CK(hipEventRecord(ev[2], s0)); gemm(v.fk, C);
+                CK(hipEventRecord(ev[2], s0)); gemm(v.g, C);
                 CK(hipEventRecord(ev[3], s0)); CK(hipEventSynchronize(ev[3]));
                 float x;
                 CK(hipEventElapsedTime(&x, ev[0], ev[1])); a1 += x;

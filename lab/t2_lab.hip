@@ -1,7 +1,7 @@
 // t2_lab.hip -- LAB harness for gemm_t2.h (two teams of 4 waves per 256 x 256 tile) against the product
 // gemm_i8_fm, bit-checked, timed in interleaved rounds in one process; `clock` mode: in-kernel stamps per team.
 //   build/t2_lab m n k rounds spec[,spec...] [clock]
-// spec: fm | fms (fm split-K 2) | fk (in-CU split-K, 256 x 128 regions) | t2 | t2ns | t2nl | t2np | t2late | t2s:N (team 1 sleeps N x 512 cycles) | t2p:N (team 0 at
+// spec: fm | fms (fm split-K 2, both slabs) | fmfNN (ticket-first split-K, slice 0 = NN/64 of K) | fk (in-CU split-K) | t2 | t2ns | t2nl | t2np | t2late | t2s:N (team 1 sleeps N x 512 cycles) | t2p:N (team 0 at
 //       priority 2 for its first N sub-steps) | t2sp:N:M (both)
 #include <cstdio>
 #include <cstdlib>
@@ -44,8 +44,13 @@ static Variant make(const std::string &spec) {
     Variant v{spec, nullptr, 512, 0, 0, true, nullptr, false};
     int a = 0, b = 0;
     if (spec == "fm") { v.fn = gemm_i8_fm<>; v.threads = 256; v.stamped = false; }
-    else if (spec == "fms") { v.fn = gemm_i8_fm<kEpiNone, false, true>; v.threads = 256; v.stamped = false; v.kind = 1; }
+    else if (spec == "fms") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitBoth>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fk") { v.fn = gemm_i8_fk<>; v.threads = 256; v.stamped = false; v.kind = 2; }
+    else if (spec == "fmf28") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 28>; v.threads = 256; v.stamped = false; v.kind = 1; }
+    else if (spec == "fmf30") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 30>; v.threads = 256; v.stamped = false; v.kind = 1; }
+    else if (spec == "fmf31") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31>; v.threads = 256; v.stamped = false; v.kind = 1; }
+    else if (spec == "fmf31p") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true>; v.threads = 256; v.stamped = false; v.kind = 1; }
+    else if (spec == "fmf32") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 32>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "t2") { v.fn = gemm_i8_t2<kT2Nt>; v.sfn = gemm_i8_t2<kT2Nt | kT2Stamp>; }
     else if (spec == "t2plain") { v.fn = gemm_i8_t2<0>; v.sfn = gemm_i8_t2<kT2Stamp>; }
     else if (spec == "t2ns") { v.fn = gemm_i8_t2<kT2NoStore>; v.sfn = gemm_i8_t2<kT2NoStore | kT2Stamp>; v.nostore = true; }

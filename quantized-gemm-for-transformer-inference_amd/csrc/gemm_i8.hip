@@ -86,7 +86,7 @@ int gemm_plan_info(int m, int n, int k, int *tile, const char **kernel) {
                                    : "gemm_i8_small<64> (64x64 tiles, LDS-DMA ring)";
         else
             *kernel = g.splits > 1 ? "gemm_i8_fm<split-K> (256x256 tiles, 4 waves of 128x128, fragment-major operands "
-                                     "straight to VGPRs, AGPR accumulators, int32 slabs + tickets)"
+                                     "straight to VGPRs, AGPR accumulators, ticket-first split-K: one int32 slab per tile)"
                                    : "gemm_i8_fm (256x256 tiles, 4 waves of 128x128, fragment-major operands straight to "
                                      "VGPRs, AGPR accumulators, fused dequant epilogue)";
     }
@@ -107,7 +107,9 @@ size_t gemm_scratch_bytes(int m, int n, int k) {
     const GemmPlan g = gemm_plan(m, n, k);
     if (g.splits <= 1) return 0;
     const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
-    return ticket_bytes(tiles) + (size_t)tiles * g.splits * g.tile * g.tile * 4;
+    // the 256-tile split (gemm_i8_fm, ticket-first) keeps ONE slab per tile; the small tiles one per slice
+    const int slabs = g.tile == 256 ? 1 : g.splits;
+    return ticket_bytes(tiles) + (size_t)tiles * slabs * g.tile * g.tile * 4;
 }
 
 // zeroes the ticket region ahead of a split launch.  A kernel rather than hipMemsetAsync: inside a
@@ -139,7 +141,10 @@ static hipError_t launch_timed(dim3 grid, dim3 block, hipStream_t stream, const 
 template <int kEpi>
 static hipError_t launch_v3(const GemmArgs &p, dim3 grid, hipStream_t stream) {
     if constexpr (kEpi != kEpiOutlier) {
-        if (p.splits == 2) return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, true>);
+        // ticket-first split-K, slice 0 = 31/64 of the k-steps (lab/t2_lab.hip, lab/c3d_lab.hip; profiles/
+        // r04_splitfirst_*.log: FFN-down GEMM alone 110.5 -> 105.8 us, the whole drop-in call 284.7 -> 279.7 us)
+        if (p.splits == 2)
+            return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi, false, kSplitFirst, true, 31>);
         if (p.splits > 2) return hipErrorNotSupported;  // gemm_plan never makes one (tiles in [128, 160) -> S <= 2)
     }
     return launch_timed(grid, dim3(kFmThreads), stream, p, gemm_i8_fm<kEpi>);

@@ -194,9 +194,26 @@ __device__ __forceinline__ bool splitk_arrive_fm(const GemmArgs &p, unsigned *la
     return *last == (unsigned)(S - 1);
 }
 
+// Split-K modes of gemm_i8_fm (two K slices per tile, the only split the 256-tile plan makes):
+//   kSplitBoth  : equal slices; each stores its slab and draws a ticket, the last arriver reads the other slab
+//                 (splitk_arrive_fm; rounds 2-3)
+//   kSplitFirst : (round 4) the ticket FIRST: only the slice that arrives first stores its slab (sc1 stores,
+//                 drained, block barrier) and publishes it by adding 2 to the ticket; the second arriver stores
+//                 nothing, waits for the published value (ticket == 4 in either arrival order: 0 -> 1 -> 3 -> 4 or
+//                 0 -> 1 -> 2 -> 4), then reads the slab with sc1 loads -- the write-through hand-off of
+//                 MI355X_MICROARCH.md (row 1 of the sc1 hand-off table: one lane's agent-scope add after every
+//                 storing wave's vmcnt(0) and a block barrier, an sc1 poll, sc1 loads).  Slice 0 takes kFirst64/64
+//                 of the k-steps, so it normally arrives first and its slab has landed before slice 1's loop ends:
+//                 one slab per tile instead of two, off the critical path.  The waiting slice never waits on a
+//                 block that is not running: the first arriver has already drawn its ticket.
+enum SplitMode { kSplitNone = 0, kSplitBoth = 1, kSplitFirst = 2 };
+
 // kNtC: the full-tile output stores are nontemporal (C2 bench, one box, interleaved: 11 598 vs 11 431 GEMMs/s, GEMM
 // 58.2 vs 59.5 us by events; profiles/r03_ab_nt_c.log) -- the 64-MiB tail streams past the caches
-template <int kEpi = kEpiNone, bool kI32 = false, bool kSplit = false, bool kNtC = !kI32>
+// kPairXcd (kSplitFirst only): blocks b and b + 8 share an XCD; XCD 2j takes K slice 0 and XCD 2j + 1 slice 1 of the
+// same 32 tiles (a 4 x 8 patch), so each XCD fetches 4 A + 8 B half-panels instead of 4 + 4 whole panels
+template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30,
+          bool kPairXcd = false>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
@@ -212,13 +229,26 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     // operand fetch 404.7 -> 337.6 MB but ran 127.3 us vs 122-126 (the slab then crosses XCDs)
     const int S = kSplit ? 2 : 1;  // the 256-tile plan splits in two or not at all (host checks)
     const int wid = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile = wid / S, slice = wid - tile * S;
+    int tile = wid / S, slice = wid - tile * S;
+    if constexpr (kPairXcd) {
+        static_assert(kSplit == kSplitFirst, "the XCD-pair map needs the write-through ticket-first hand-off");
+        // gridDim.x = 256 (the split plan runs at exactly 128 tiles): 32 blocks per XCD
+        const int xcd = blockIdx.x & 7;
+        tile = (xcd >> 1) * 32 + (blockIdx.x >> 3);
+        slice = xcd & 1;
+    }
     int tm, tn;
     group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
     const int nsub = (int)(p.k_pad / 64);
-    // this slice's sub-steps [u0, u0 + nloc) of the nsub 64-deep k-blocks
-    const int u0 = __builtin_amdgcn_readfirstlane(slice * nsub / S);
-    const int nloc = __builtin_amdgcn_readfirstlane((slice + 1) * nsub / S - u0);
+    // this slice's sub-steps [u0, u0 + nloc) of the nsub 64-deep k-blocks (kSplitFirst: slice 0 the shorter one)
+    int cut = slice * nsub / S, end = (slice + 1) * nsub / S;
+    if constexpr (kSplit == kSplitFirst) {
+        const int n0 = min(max(nsub * kFirst64 / 64, 1), nsub - 1);
+        cut = slice ? n0 : 0;
+        end = slice ? nsub : n0;
+    }
+    const int u0 = __builtin_amdgcn_readfirstlane(cut);
+    const int nloc = __builtin_amdgcn_readfirstlane(end - cut);
     // this wave's half panels: 8 row groups x nsub blocks each (= 128 packed rows), from block u0 on
     const int half_bytes = 8 * nsub * 1024 - u0 * 1024;
     const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
@@ -280,7 +310,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     }
     // the last MFMAs' results are read by VALU below; the asm statements hide them from hipcc's padding
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-    if constexpr (kSplit) {
+    if constexpr (kSplit == kSplitBoth) {
         {
             // split-K: slabs + arrival ticket (write-through form, see splitk_combine); the last slice of
             // the tile holds the complete sums and runs the epilogue
@@ -288,6 +318,34 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
             if (!splitk_arrive_fm(p, last, acc, tile, slice, wave, lane, tid)) return;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: slab loads stay below
         }
+    } else if constexpr (kSplit == kSplitFirst) {
+        unsigned *last = reinterpret_cast<unsigned *>(lds + 4 * kBlockBytes + 2048);
+        if (tid == 0) *last = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (*last == 0u) {
+            // first arriver: this slice's sums to the tile's ONE slab (write-through), then publish
+            constexpr int kSlabBytes = 4 * 8 * 8 * 64 * 16;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char *>(p.slabs) + (int64_t)tile * kSlabBytes,
+                                                              0, kSlabBytes, 0x00020000);
+            const int lane_off = (wave * 64 * 64 + lane) * 16;
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 8; ++ni)
+                    __builtin_amdgcn_raw_buffer_store_b128(acc[mi][ni], rs, lane_off + (mi * 8 + ni) * 1024, 0, 16 /* sc1 */);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(p.tickets + tile, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        // second arriver: wait for the published slab (its producer drew its ticket before this block did)
+        if (tid == 0) {
+            while (__hip_atomic_load(p.tickets + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 4u)
+                __builtin_amdgcn_s_sleep(2);
+            if (p.reset_tickets) __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: slab loads stay below
     }
 
     const int gi0 = tm * BM, gj0 = tn * BN;
@@ -339,8 +397,9 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         if constexpr (kSplit) {
             constexpr int kSlabBytes = 4 * 8 * 8 * 64 * 16;
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<char *>(p.slabs) + ((int64_t)tile * 2 + (1 - slice)) * kSlabBytes, 0, kSlabBytes,
-                0x00020000);
+                reinterpret_cast<char *>(p.slabs) +
+                    (kSplit == kSplitFirst ? (int64_t)tile : (int64_t)tile * 2 + (1 - slice)) * kSlabBytes,
+                0, kSlabBytes, 0x00020000);
             const int lane_off = (wave * 64 * 64 + lane) * 16;
 #pragma unroll
             for (int mq = 0; mq < 4; ++mq)

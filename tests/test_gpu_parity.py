@@ -217,10 +217,11 @@ def test_long_k_drop_in(qg, oracle, device, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(2048, 4096, 2048), (1900, 4000, 3000), (1800, 4096, 4500)])
 def test_256_tile_split_k_plans(qg, oracle, device, M, N, K):
-    """128 tiles of 256 x 256 with K >= 2048: the split-K plan (S = 2) on gemm_i8_fm -- slabs stored
-    write-through from the AGPR accumulators, the last slice of each tile adds the other slab and runs the
-    epilogue.  Ragged M / N / K edges, K > 4096 (two-pass pack); library scratch twice, then a caller
-    workspace full of 0xFF (tickets zeroed by the pack launch)."""
+    """128 tiles of 256 x 256 with K >= 2048: the split-K plan (S = 2) on gemm_i8_fm, ticket-first (round 4) --
+    the slice that draws the ticket first stores its slab write-through from the AGPR accumulators and publishes
+    it; the other adds it and runs the epilogue.  Ragged M / N / K edges, K > 4096 (two-pass pack); library
+    scratch twice (the second arriver resets the ticket), then a caller workspace full of 0xFF (tickets zeroed by
+    the pack launch)."""
     L = qg.load()
     assert L.qgemm_gemm_plan(M, N, K, None, None) == 2, "shape expected to run the 256-tile split-K plan"
     X, W = oracle.inputs(M, N, K, 131)
@@ -239,6 +240,25 @@ def test_256_tile_split_k_plans(qg, oracle, device, M, N, K):
                                ws.data_ptr(), ws.numel(), qg._stream(device)) == 0
     torch.cuda.synchronize()
     assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} caller workspace")
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 4096, 2048), (2048, 4096, 16384)])
+def test_256_tile_split_k_ticket_first_repeat(qg, oracle, device, M, N, K):
+    """Race screen of the ticket-first split-K hand-off (gemm_i8_fm<kSplitFirst>): 20 back-to-back calls on the
+    library scratch (each second arriver polls for the first's publish, then resets the ticket for the next
+    launch), every output bit of every call.  The slices of a tile finish within a few microseconds of each
+    other, so both arrival orders occur; K = 2048 makes the two slices nearly equal (15 and 17 sub-steps)."""
+    L = qg.load()
+    assert L.qgemm_gemm_plan(M, N, K, None, None) == 2
+    X, W = oracle.inputs(M, N, K, 57)
+    want = oracle.quantized_mm(X, W)
+    pa, pb = qg.pack_a(_dev(X, device)), qg.pack_b(_dev(W, device))
+    outs = [torch.full((M, N), float("nan"), device=device) for _ in range(20)]
+    for O in outs:
+        qg.mm_packed(pa, pb, O)
+    torch.cuda.synchronize()
+    for i, O in enumerate(outs):
+        assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} repeat {i}")
 
 
 def test_device_generator_matches_oracle(qg, oracle, device):
