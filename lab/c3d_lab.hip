@@ -1,9 +1,8 @@
 // c3d_lab.hip -- LAB harness: the whole FFN-down drop-in call (BASELINE configs[2], X 2048 x 16384, W 16384 x 4096)
 // as the library runs it -- pass 1 (X rows + W column maxima), pass 2 (W re-read, quantized, transposed), the int8
 // GEMM -- with the sweep orders and the GEMM as variables, every output bit compared with the library's order:
-//   P1 W-first (library) | X-first (W's column-max sweep last: W's bottom rows are the most recent bytes in the
-//      Infinity Cache when pass 2 starts)
-//   P2 fwd (library, top rows first) | rev (bottom rows first: re-reads what pass 1 read last)
+//   order 0: pass 1 W-first, pass 2 forward (round 3); 1: pass 1 X-first, pass 2 bottom-up (re-reads what pass 1
+//      read last; round 4 product); 2: pass 1 W only, pass 2 bottom-up with X's rows at its end
 //   G  gemm_i8_fm split-K 2 with both slabs (rounds 2-3) | ticket-first (one slab, uneven K split: round 4) |
 //      fk (gemm_i8_fk: split-K inside the CU)
 //   build/c3d_lab m n k rounds
@@ -39,19 +38,28 @@ int main(int argc, char **argv) {
     hipStream_t s0; CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
     const int col_blocks = (n + kColBlock - 1) / kColBlock, ncol = col_blocks * (int)vw.parts, nrow = (int)vx.rows_pad;
     const float range = 127.f;
-    auto pass1 = [&](bool xf) {
-        if (xf)
+    // order: 0 = W-first pass 1, forward pass 2 (round 3); 1 = X-first pass 1, pass 2 bottom-up (round 4 product);
+    // 2 = W-only pass 1 (colmax_kernel), pass 2 bottom-up with X's rows at its end (pack_cols_then_rows_kernel)
+    auto pass1 = [&](int order) {
+        if (order == 2) {
+            colmax_kernel<true><<<dim3(col_blocks, (unsigned)vw.parts), 256, 0, s0>>>(W, n, k, n, vw.scratch, vw.rows_pad);
+        } else if (order == 1) {
             pack_rows_and_colmax_kernel<-1, true><<<ncol + nrow, 256, 0, s0>>>(
                 X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n, n, vw.scratch, vw.rows_pad, col_blocks, ncol,
                 range, reinterpret_cast<uint32_t *>(tickets), 1024);
-        else
+        } else {
             pack_rows_and_colmax_kernel<-1, false><<<ncol + nrow, 256, 0, s0>>>(
                 X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n, n, vw.scratch, vw.rows_pad, col_blocks, ncol,
                 range, reinterpret_cast<uint32_t *>(tickets), 1024);
+        }
     };
     const dim3 g2((unsigned)(vw.rows_pad / kTc), (unsigned)((vw.k_pad / kTk + kTilesPerBlock - 1) / kTilesPerBlock));
-    auto pass2 = [&](bool rev) {
-        if (rev)
+    auto pass2 = [&](int order) {
+        if (order == 2)
+            pack_cols_then_rows_kernel<<<g2.x * g2.y + nrow, 256, 0, s0>>>(
+                W, n, k, n, range, vw.scratch, vw.parts, vw.rows_pad, vw.scale, vw.q, vw.k_pad, (int)g2.x, (int)g2.y, X, k,
+                m, vx.scale, vx.q, vx.rows_pad, reinterpret_cast<uint32_t *>(tickets), 1024);
+        else if (order == 1)
             pack_cols_kernel<true, kTilesPerBlock, true><<<g2, 256, 0, s0>>>(W, n, k, n, range, vw.scratch, vw.parts,
                                                                              vw.rows_pad, vw.scale, vw.q, vw.k_pad);
         else
@@ -75,21 +83,18 @@ int main(int argc, char **argv) {
         if (g == 2) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31><<<tiles * 2, 256, 0, s0>>>(p);
         if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);
     };
-    struct V { std::string name; bool xf, rev; int g; };
-    std::vector<V> vs;
-    const char *gn[5] = {"_both", "_first30", "_first31", "_fk", "_first31pair"};
-    for (int g : {0, 2, 4})
-        for (int a = 0; a < 2; ++a)
-            vs.push_back({std::string(a ? "xfirst_rev" : "wfirst_fwd") + gn[g], a != 0, a != 0, g});
+    struct V { std::string name; int order; int g; };
+    std::vector<V> vs = {{"wfirst_fwd_first31", 0, 2}, {"xfirst_rev_first31", 1, 2}, {"wonly_revxrows_first31", 2, 2},
+                         {"xfirst_rev_both", 1, 0}};
     // reference: the library's order
-    pass1(false); pass2(false); gemm(0, Cref);
+    pass1(0); pass2(0); gemm(0, Cref);
     CK(hipStreamSynchronize(s0));
     std::vector<float> href((size_t)m * n), hgot(href.size());
     CK(hipMemcpy(href.data(), Cref, href.size() * 4, hipMemcpyDeviceToHost));
     for (auto &v : vs) {
         CK(hipMemsetAsync(C, 0xff, (size_t)m * n * 4, s0));
         CK(hipMemsetAsync(vw.q, 0x5a, vw.rows_pad * vw.k_pad, s0));
-        pass1(v.xf); pass2(v.rev); gemm(v.g, C);
+        pass1(v.order); pass2(v.order); gemm(v.g, C);
         CK(hipStreamSynchronize(s0));
         CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
         printf("check %-18s %s\n", v.name.c_str(), memcmp(href.data(), hgot.data(), href.size() * 4) ? "DIFF" : "same");
@@ -98,15 +103,15 @@ int main(int argc, char **argv) {
     hipEvent_t ev[4];
     for (auto &e : ev) CK(hipEventCreate(&e));
     std::vector<std::vector<float>> tc(vs.size()), t1(vs.size()), t2(vs.size()), tg(vs.size());
-    for (int i = 0; i < 300; ++i) { pass1(false); pass2(false); gemm(0, C); }  // clocks up
+    for (int i = 0; i < 300; ++i) { pass1(1); pass2(1); gemm(2, C); }  // clocks up
     for (int r = 0; r < rounds; ++r)
         for (size_t i = 0; i < vs.size(); ++i) {
             const V &v = vs[i];
-            for (int w = 0; w < 3; ++w) { pass1(v.xf); pass2(v.rev); gemm(v.g, C); }
+            for (int w = 0; w < 3; ++w) { pass1(v.order); pass2(v.order); gemm(v.g, C); }
             float a1 = 0, a2 = 0, ag = 0, ac = 0;
             for (int j = 0; j < reps; ++j) {
-                CK(hipEventRecord(ev[0], s0)); pass1(v.xf);
-                CK(hipEventRecord(ev[1], s0)); pass2(v.rev);
+                CK(hipEventRecord(ev[0], s0)); pass1(v.order);
+                CK(hipEventRecord(ev[1], s0)); pass2(v.order);
                 CK(hipEventRecord(ev[2], s0)); gemm(v.g, C);
                 CK(hipEventRecord(ev[3], s0)); CK(hipEventSynchronize(ev[3]));
                 float x;

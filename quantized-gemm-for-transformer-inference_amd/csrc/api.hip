@@ -194,11 +194,8 @@ int op_mm_quantize_ws(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
         hipError_t e = launch_pack_single_pass(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s, tickets, ntickets);
         if (e == hipSuccess) return gemm(true);
         if (e != hipErrorNotSupported) return err(e);
-        e = launch_pack_rows_and_colmax(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s, tickets, ntickets);
-        if (e == hipSuccess) {
-            if ((e = launch_pack_cols_pass2(B, b_stride_h, k, n, range, vb, s)) != hipSuccess) return err(e);
-            return gemm(true);
-        }
+        e = launch_pack_two_pass(A, a_stride_h, m, k, va, B, b_stride_h, n, vb, range, s, tickets, ntickets);
+        if (e == hipSuccess) return gemm(true);
         if (e != hipErrorNotSupported) return err(e);
     }
     int rc = qgemm_pack_a(A, a_stride_h, a_stride_w, m, k, range, pa, stream);

@@ -522,17 +522,17 @@ constexpr int kTilesPerBlock = 8;
 
 // kRev: the k-ranges in reverse dispatch order (bottom rows of W first): pass 1 swept W top to bottom, so its
 // last rows are the ones still in the Infinity Cache
-template <bool VEC, int kTPB = kTilesPerBlock, bool kRev = false>
-__global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
-                                                        float range, const uint32_t *__restrict__ partial,
-                                                        int64_t parts, int64_t rows_pad, float *__restrict__ scale,
-                                                        int8_t *__restrict__ q, int64_t k_pad) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[2][kTc * kTStride];  // [64 packed rows][132 B], 2 buffers
-    __shared__ float s_sh[kTc];
+// block (bx, by): packed rows [64 bx, 64 bx + 64) x k-tiles [kTPB by, kTPB by + kTPB); tile = 2 x kTc x kTStride
+// bytes of LDS (two [64 packed rows][132 B] buffers), s_sh = kTc floats
+template <bool VEC, int kTPB>
+__device__ __forceinline__ void pack_cols_body(int bx, int by, const float *__restrict__ src, int64_t sh, int len,
+                                               int cols, float range, const uint32_t *__restrict__ partial,
+                                               int64_t parts, int64_t rows_pad, float *__restrict__ scale,
+                                               int8_t *__restrict__ q, int64_t k_pad, uint8_t (*tile)[kTc * kTStride],
+                                               float *s_sh) {
     const int t = threadIdx.x;
-    const int64_t n0 = (int64_t)blockIdx.x * kTc;
+    const int64_t n0 = (int64_t)bx * kTc;
     const int64_t nkt = k_pad / kTk;
-    const int by = kRev ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
     const int64_t kt0 = (int64_t)by * kTPB;
     const int64_t kt1 = min(nkt, kt0 + kTPB);
     const int col4 = t & 15;  // 4 input columns n0 + 4*col4 .. +3
@@ -593,6 +593,42 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[h][i] = xn[h][i];
+    }
+}
+
+template <bool VEC, int kTPB = kTilesPerBlock, bool kRev = false>
+__global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict__ src, int64_t sh, int len, int cols,
+                                                        float range, const uint32_t *__restrict__ partial,
+                                                        int64_t parts, int64_t rows_pad, float *__restrict__ scale,
+                                                        int8_t *__restrict__ q, int64_t k_pad) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[2][kTc * kTStride];  // [64 packed rows][132 B], 2 buffers
+    __shared__ float s_sh[kTc];
+    const int by = kRev ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
+    pack_cols_body<VEC, kTPB>(blockIdx.x, by, src, sh, len, cols, range, partial, parts, rows_pad, scale, q, k_pad, tile,
+                              s_sh);
+}
+
+// Pass 2 of the long-row two-pass pack (4096 < K <= 16384, round 4) with X's rows packed at its END: blocks
+// [0, gx * gy) run pack_cols bottom-up (the rows a W-only pass 1 read last first: they are still in the Infinity
+// Cache), blocks [gx * gy, + rows_pad) one X row each (pack_row_block_body); block 0 zeroes zero_words (the GEMM's
+// split-K tickets).  Pass 1 is colmax_kernel alone: a clean sweep of W.  lab/c3d_lab.hip, FFN down, one box,
+// interleaved (profiles/r04_c3d_xrows.log): passes 97.3 + 63.5 -> 50.9 + 95.2 us, call 281.2 -> 267.5 us; the GEMM
+// after it unchanged (121.3 vs 120.3 us).
+__global__ __launch_bounds__(256) void pack_cols_then_rows_kernel(
+    const float *__restrict__ w, int64_t wsh, int k, int n, float range, const uint32_t *__restrict__ partial,
+    int64_t parts, int64_t w_rows_pad, float *__restrict__ w_scale, int8_t *__restrict__ w_q, int64_t k_pad, int gx,
+    int gy, const float *__restrict__ x, int64_t xsh, int m, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
+    int64_t x_rows_pad, uint32_t *zero_words, int nzero) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[2][kTc * kTStride];
+    __shared__ float s_sh[kTc];
+    zero_words_block0(zero_words, nzero);
+    const int bid = blockIdx.x, ncb = gx * gy;
+    if (bid < ncb) {
+        pack_cols_body<true, kTilesPerBlock>(bid % gx, gy - 1 - bid / gx, w, wsh, k, n, range, partial, parts, w_rows_pad,
+                                             w_scale, w_q, k_pad, tile, s_sh);
+    } else {
+        pack_row_block_body(xcd_contig(bid, ncb, (int)gridDim.x - ncb), x, xsh, m, k, range, x_scale, x_q, x_rows_pad,
+                            k_pad, s_sh);
     }
 }
 
@@ -1284,6 +1320,28 @@ hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float l
     if (blocks > 8192) blocks = 8192;
     fill_uniform_kernel<<<(unsigned)blocks, 256, 0, stream>>>(dst, count, seed, lo, hi);
     return hipGetLastError();
+}
+
+hipError_t launch_pack_two_pass(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b, int64_t bsh,
+                                int n, PackedView outb, float range, hipStream_t stream, uint32_t *zero_words, int nzero) {
+    if (k < 2 || !rows_vec_ok(a, ash, 1, m) || !cols_vec_ok(b, bsh, n)) return hipErrorNotSupported;
+    if (rows_regs(k) < 0) {
+        // long rows: W-only pass 1 (column maxima), then pass 2 bottom-up with X's rows at its end
+        const int col_blocks = (n + kColBlock - 1) / kColBlock;
+        colmax_kernel<true><<<dim3((unsigned)col_blocks, (unsigned)outb.parts), 256, 0, stream>>>(b, bsh, k, n, outb.scratch,
+                                                                                               outb.rows_pad);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const unsigned gx = (unsigned)(outb.rows_pad / kTc);
+        const unsigned gy = (unsigned)((outb.k_pad / kTk + kTilesPerBlock - 1) / kTilesPerBlock);
+        pack_cols_then_rows_kernel<<<gx * gy + (unsigned)outa.rows_pad, 256, 0, stream>>>(
+            b, bsh, k, n, range, outb.scratch, outb.parts, outb.rows_pad, outb.scale, outb.q, outb.k_pad, (int)gx, (int)gy,
+            a, ash, m, outa.scale, outa.q, outa.rows_pad, zero_words, nzero);
+        return hipGetLastError();
+    }
+    hipError_t e = launch_pack_rows_and_colmax(a, ash, m, k, outa, b, bsh, n, outb, range, stream, zero_words, nzero);
+    if (e != hipSuccess) return e;
+    return launch_pack_cols_pass2(b, bsh, k, n, range, outb, stream);
 }
 
 hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,

@@ -118,6 +118,12 @@ hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, 
                             PackedView out, hipStream_t stream);
 hipError_t launch_pack_cols(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                             hipStream_t stream);
+// The two-pass pack of a row-major A and B (B's columns reduced in pass 1, quantized in pass 2; A's rows in one of
+// the passes): long rows (4096 < K <= 16384) as a W-only pass 1 + pass 2 with A's rows at its end, shorter rows as
+// launch_pack_rows_and_colmax + launch_pack_cols_pass2.  hipErrorNotSupported when the layouts do not allow it.
+hipError_t launch_pack_two_pass(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b, int64_t bsh,
+                                int n, PackedView outb, float range, hipStream_t stream, uint32_t *zero_words = nullptr,
+                                int nzero = 0);
 // One launch: pack_rows of a row-major A (vector path) and pass 1 of pack_cols of a row-major B.
 // Returns hipErrorNotSupported when the layouts do not allow it (caller falls back).
 hipError_t launch_pack_rows_and_colmax(const float *a, int64_t ash, int m, int k, PackedView outa, const float *b,

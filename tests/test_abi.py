@@ -54,8 +54,8 @@ def test_version_and_sizes_without_gpu(qg):
         assert L.qgemm_packed_size(rows, k) == size(rows, k), (rows, k)
     ws = L.op_mm_quantize_workspace_size(4096, 4096, 4096)
     assert ws == 2 * size(4096, 4096)  # 256 tiles: no split-K scratch
-    # FFN down (2048 x 16384 -> 4096): 128 tiles, split-K 2 -> tickets + 128 x 2 int32 256x256 slabs
-    split = 4096 + 128 * 2 * 256 * 256 * 4
+    # FFN down (2048 x 16384 -> 4096): 128 tiles, split-K 2, ticket-first -> tickets + ONE int32 256x256 slab per tile
+    split = 4096 + 128 * 256 * 256 * 4
     assert L.op_mm_quantize_workspace_size(2048, 4096, 16384) == split + size(2048, 16384) + size(4096, 16384)
     assert L.op_mm_quantize_workspace_size(4, 4, 0) == 0
 
