@@ -44,6 +44,7 @@ static Variant make(const std::string &spec) {
     Variant v{spec, nullptr, 512, 0, 0, true, nullptr, false};
     int a = 0, b = 0;
     if (spec == "fm") { v.fn = gemm_i8_fm<>; v.threads = 256; v.stamped = false; }
+    else if (spec == "fmrot") { v.fn = gemm_i8_fm<>; v.threads = 256; v.stamped = false; v.kind = 3; }
     else if (spec == "fms") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitBoth>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fk") { v.fn = gemm_i8_fk<>; v.threads = 256; v.stamped = false; v.kind = 2; }
     else if (spec == "fmf28") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 28>; v.threads = 256; v.stamped = false; v.kind = 1; }
@@ -105,9 +106,10 @@ int main(int argc, char **argv) {
         GemmArgs q = p;
         if (v.kind == 1) { q.splits = 2; q.slabs = slabs; q.tickets = tickets; q.reset_tickets = 1; }
         if (v.kind == 2) q.tiles_n = n / 128;
+        if (v.kind == 3) q.rot_rows = 1;
         return q;
     };
-    auto grid_of = [&](const Variant &v) { return dim3(v.kind ? nb * 2 : nb); };
+    auto grid_of = [&](const Variant &v) { return dim3(v.kind == 1 || v.kind == 2 ? nb * 2 : nb); };
 
     if (clock) {
         unsigned long long *sym;

@@ -173,6 +173,8 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, g.tiles_m, g.tiles_n,
                inv_r2, 1, nullptr, nullptr, bias, tickets_zeroed ? 1 : 0};
     const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
+    // output rows of >= 64 KiB (FFN up's 16 384 columns): rotate each 256-tile's row-store order (gemm_i8_fm)
+    p.rot_rows = (csw == 1 && csh >= 16384) ? 1 : 0;
     if (g.splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
         p.splits = g.splits;
         p.tickets = static_cast<unsigned *>(scratch);

@@ -68,6 +68,9 @@ struct GemmArgs {
     const float *wo;
     const int *ocount;
     int64_t wo_ld;
+    // gemm_i8_fm's full-tile stores: each tile starts its row-pair loop at its own offset (set by the host for
+    // output rows of >= 64 KiB, where the tiles' concurrent row writes otherwise meet on the same memory channels)
+    int rot_rows;
 };
 
 // Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
@@ -381,6 +384,9 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     float *T = reinterpret_cast<float *>(lds + wave * kBlockBytes);
     const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
                       gj0 + BN <= p.n && gi0 + BM <= p.m;
+    // row-pair rotation of the full-tile stores (lab/w4_lab.hip `stride` mode, profiles/r03_f4_store_order_lab.log:
+    // FFN-up output, 64-KiB rows, 121.6 -> 118.2 us; at 16-KiB rows it cost the 8192-row shard 2 us, hence host-set)
+    const int rot = __builtin_amdgcn_readfirstlane(p.rot_rows ? ((tn * 7 + tm * 3) & 31) : 0);
     // the scales (and bias) into registers first: T and the scales share the one LDS array, so a scale read
     // between T stores would be re-issued and waited for after every store
     float cwv[8], bv[8];
@@ -483,7 +489,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         if (full) {
 #pragma unroll 8
             for (int it = 0; it < 32; ++it) {
-                const int rr = 2 * it + (lane >> 5);
+                const int rr = 2 * ((it + rot) & 31) + (lane >> 5);
                 const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
                 float4 *dst = reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4);
                 if constexpr (kNtC) {
