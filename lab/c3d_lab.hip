@@ -2,7 +2,8 @@
 // as the library runs it -- pass 1 (X rows + W column maxima), pass 2 (W re-read, quantized, transposed), the int8
 // GEMM -- with the sweep orders and the GEMM as variables, every output bit compared with the library's order:
 //   order 0: pass 1 W-first, pass 2 forward (round 3); 1: pass 1 X-first, pass 2 bottom-up (re-reads what pass 1
-//      read last; round 4 product); 2: pass 1 W only, pass 2 bottom-up with X's rows at its end
+//      read last); 2: pass 1 W only, pass 2 bottom-up with X's rows at its end (round 4 product); 3: order 2 with
+//      non-temporal loads of W and X in pass 2; 4: order 2 with non-temporal loads of X only
 //   G  gemm_i8_fm split-K 2 with both slabs (rounds 2-3) | ticket-first (one slab, uneven K split: round 4) |
 //      fk (gemm_i8_fk: split-K inside the CU)
 //   build/c3d_lab m n k rounds
@@ -41,7 +42,7 @@ int main(int argc, char **argv) {
     // order: 0 = W-first pass 1, forward pass 2 (round 3); 1 = X-first pass 1, pass 2 bottom-up (round 4 product);
     // 2 = W-only pass 1 (colmax_kernel), pass 2 bottom-up with X's rows at its end (pack_cols_then_rows_kernel)
     auto pass1 = [&](int order) {
-        if (order == 2) {
+        if (order >= 2) {
             colmax_kernel<true><<<dim3(col_blocks, (unsigned)vw.parts), 256, 0, s0>>>(W, n, k, n, vw.scratch, vw.rows_pad);
         } else if (order == 1) {
             pack_rows_and_colmax_kernel<-1, true><<<ncol + nrow, 256, 0, s0>>>(
@@ -55,7 +56,15 @@ int main(int argc, char **argv) {
     };
     const dim3 g2((unsigned)(vw.rows_pad / kTc), (unsigned)((vw.k_pad / kTk + kTilesPerBlock - 1) / kTilesPerBlock));
     auto pass2 = [&](int order) {
-        if (order == 2)
+        if (order == 3)
+            pack_cols_then_rows_kernel<true, true><<<g2.x * g2.y + nrow, 256, 0, s0>>>(
+                W, n, k, n, range, vw.scratch, vw.parts, vw.rows_pad, vw.scale, vw.q, vw.k_pad, (int)g2.x, (int)g2.y, X, k,
+                m, vx.scale, vx.q, vx.rows_pad, reinterpret_cast<uint32_t *>(tickets), 1024);
+        else if (order == 4)
+            pack_cols_then_rows_kernel<false, true><<<g2.x * g2.y + nrow, 256, 0, s0>>>(
+                W, n, k, n, range, vw.scratch, vw.parts, vw.rows_pad, vw.scale, vw.q, vw.k_pad, (int)g2.x, (int)g2.y, X, k,
+                m, vx.scale, vx.q, vx.rows_pad, reinterpret_cast<uint32_t *>(tickets), 1024);
+        else if (order == 2)
             pack_cols_then_rows_kernel<<<g2.x * g2.y + nrow, 256, 0, s0>>>(
                 W, n, k, n, range, vw.scratch, vw.parts, vw.rows_pad, vw.scale, vw.q, vw.k_pad, (int)g2.x, (int)g2.y, X, k,
                 m, vx.scale, vx.q, vx.rows_pad, reinterpret_cast<uint32_t *>(tickets), 1024);
@@ -84,8 +93,7 @@ int main(int argc, char **argv) {
         if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);
     };
     struct V { std::string name; int order; int g; };
-    std::vector<V> vs = {{"wfirst_fwd_first31", 0, 2}, {"xfirst_rev_first31", 1, 2}, {"wonly_revxrows_first31", 2, 2},
-                         {"xfirst_rev_both", 1, 0}};
+    std::vector<V> vs = {{"product", 2, 2}, {"nt_w_x", 3, 2}, {"nt_x", 4, 2}};
     // reference: the library's order
     pass1(0); pass2(0); gemm(0, Cref);
     CK(hipStreamSynchronize(s0));
@@ -103,7 +111,7 @@ int main(int argc, char **argv) {
     hipEvent_t ev[4];
     for (auto &e : ev) CK(hipEventCreate(&e));
     std::vector<std::vector<float>> tc(vs.size()), t1(vs.size()), t2(vs.size()), tg(vs.size());
-    for (int i = 0; i < 300; ++i) { pass1(1); pass2(1); gemm(2, C); }  // clocks up
+    for (int i = 0; i < 300; ++i) { pass1(2); pass2(2); gemm(2, C); }  // clocks up
     for (int r = 0; r < rounds; ++r)
         for (size_t i = 0; i < vs.size(); ++i) {
             const V &v = vs[i];

@@ -86,6 +86,18 @@ __device__ __forceinline__ void st_f32(float *p, float v) {
     else *p = v;
 }
 
+// 16-B load; kNt: non-temporal (the line is not kept in the Infinity Cache for a later reader)
+template <bool kNt>
+__device__ __forceinline__ float4 ld_f4(const float *p) {
+    if constexpr (kNt) {
+        typedef float v4f_nt __attribute__((ext_vector_type(4)));
+        const v4f_nt v = __builtin_nontemporal_load(reinterpret_cast<const v4f_nt *>(p));
+        return make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        return *reinterpret_cast<const float4 *>(p);
+    }
+}
+
 // Blocks b and b + 8 run on one XCD.  For a role occupying blocks [base, base + count): a role-local index
 // that gives every XCD ONE contiguous range (bijective).  Row packs index their rows with it: a 128-B line
 // of the fragment-major q holds 16-B pieces of 8 consecutive rows (qgemm_internal.h fofs), and rows packed
@@ -285,6 +297,7 @@ __device__ __forceinline__ void write_staged_rows(const uint32_t *stage, int rsw
 // thread in registers (4-KiB coalesced loads per block instruction), block-wide absmax (shuffle + LDS),
 // quantized from the registers -- one HBM read of the row.  `red` holds >= 5 floats of LDS.
 constexpr int kLongRowMax = 16384;
+template <bool kNt = false>
 __device__ __forceinline__ void pack_row_block_body(int64_t row, const float *__restrict__ src, int64_t sh, int rows,
                                                     int len, float range, float *__restrict__ scale,
                                                     int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
@@ -299,13 +312,12 @@ __device__ __forceinline__ void pack_row_block_body(int64_t row, const float *__
         return;
     }
     const float *srow = src + row * sh;
-    const float4 *s4 = reinterpret_cast<const float4 *>(srow);
     const int nfull = len >> 2;
     float4 v[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int c = t + 256 * j;
-        v[j] = (c < nfull) ? s4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[j] = (c < nfull) ? ld_f4<kNt>(srow + 4 * (int64_t)c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     float p = -INFINITY;
 #pragma unroll
@@ -490,7 +502,7 @@ constexpr int kTc = 64;             // output rows (= input columns) per block
 constexpr int kTk = 128;            // k per block
 constexpr int kTStride = kTk + 4;   // LDS row stride: 33 dwords (odd) -> transpose writes 2-way, reads conflict-free
 
-template <bool VEC>
+template <bool VEC, bool kNt = false>
 __device__ __forceinline__ void load_col_tile(float4 (&x)[2][4], const float *__restrict__ src, int64_t sh, int len,
                                               int cols, int64_t c, int64_t k0, int rg) {
 #pragma unroll
@@ -502,7 +514,7 @@ __device__ __forceinline__ void load_col_tile(float4 (&x)[2][4], const float *__
             if (kk < len) {
                 const float *rp = src + kk * sh + c;
                 if constexpr (VEC) {
-                    if (c < cols) v = *reinterpret_cast<const float4 *>(rp);
+                    if (c < cols) v = ld_f4<kNt>(rp);
                 } else {
                     if (c + 0 < cols) v.x = rp[0];
                     if (c + 1 < cols) v.y = rp[1];
@@ -524,7 +536,7 @@ constexpr int kTilesPerBlock = 8;
 // last rows are the ones still in the Infinity Cache
 // block (bx, by): packed rows [64 bx, 64 bx + 64) x k-tiles [kTPB by, kTPB by + kTPB); tile = 2 x kTc x kTStride
 // bytes of LDS (two [64 packed rows][132 B] buffers), s_sh = kTc floats
-template <bool VEC, int kTPB>
+template <bool VEC, int kTPB, bool kNt = false>
 __device__ __forceinline__ void pack_cols_body(int bx, int by, const float *__restrict__ src, int64_t sh, int len,
                                                int cols, float range, const uint32_t *__restrict__ partial,
                                                int64_t parts, int64_t rows_pad, float *__restrict__ scale,
@@ -540,7 +552,7 @@ __device__ __forceinline__ void pack_cols_body(int bx, int by, const float *__re
     const int64_t c = n0 + 4 * col4;
     // first tile's loads before the scale reduction (their latency overlaps it)
     float4 x[2][4], xn[2][4];
-    load_col_tile<VEC>(x, src, sh, len, cols, c, kt0 * kTk, rg);
+    load_col_tile<VEC, kNt>(x, src, sh, len, cols, c, kt0 * kTk, rg);
     if (t < kTc) {
         const int64_t j = n0 + t;
         float cx = 0.0f, s = 0.0f;
@@ -560,7 +572,7 @@ __device__ __forceinline__ void pack_cols_body(int bx, int by, const float *__re
     const int kc = (t & 3) * 32;  // byte offset within the 128-byte k slice
     for (int64_t kt = kt0; kt < kt1; ++kt) {
         const int64_t k0 = kt * kTk;
-        if (kt + 1 < kt1) load_col_tile<VEC>(xn, src, sh, len, cols, c, k0 + kTk, rg);
+        if (kt + 1 < kt1) load_col_tile<VEC, kNt>(xn, src, sh, len, cols, c, k0 + kTk, rg);
         uint8_t *tb = tile[(kt - kt0) & 1];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -614,6 +626,7 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
 // split-K tickets).  Pass 1 is colmax_kernel alone: a clean sweep of W.  lab/c3d_lab.hip, FFN down, one box,
 // interleaved (profiles/r04_c3d_xrows.log): passes 97.3 + 63.5 -> 50.9 + 95.2 us, call 281.2 -> 267.5 us; the GEMM
 // after it unchanged (121.3 vs 120.3 us).
+template <bool kNtW = false, bool kNtX = false>
 __global__ __launch_bounds__(256) void pack_cols_then_rows_kernel(
     const float *__restrict__ w, int64_t wsh, int k, int n, float range, const uint32_t *__restrict__ partial,
     int64_t parts, int64_t w_rows_pad, float *__restrict__ w_scale, int8_t *__restrict__ w_q, int64_t k_pad, int gx,
@@ -624,10 +637,10 @@ __global__ __launch_bounds__(256) void pack_cols_then_rows_kernel(
     zero_words_block0(zero_words, nzero);
     const int bid = blockIdx.x, ncb = gx * gy;
     if (bid < ncb) {
-        pack_cols_body<true, kTilesPerBlock>(bid % gx, gy - 1 - bid / gx, w, wsh, k, n, range, partial, parts, w_rows_pad,
-                                             w_scale, w_q, k_pad, tile, s_sh);
+        pack_cols_body<true, kTilesPerBlock, kNtW>(bid % gx, gy - 1 - bid / gx, w, wsh, k, n, range, partial, parts,
+                                                   w_rows_pad, w_scale, w_q, k_pad, tile, s_sh);
     } else {
-        pack_row_block_body(xcd_contig(bid, ncb, (int)gridDim.x - ncb), x, xsh, m, k, range, x_scale, x_q, x_rows_pad,
+        pack_row_block_body<kNtX>(xcd_contig(bid, ncb, (int)gridDim.x - ncb), x, xsh, m, k, range, x_scale, x_q, x_rows_pad,
                             k_pad, s_sh);
     }
 }
@@ -786,6 +799,9 @@ constexpr int kW32LdsBytes = kW32LdsI * 4 * 16 * 1024;  // [i][e][wave] x 1 KiB
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// kAux: cache-policy bits of W's loads (0: default; 2: non-temporal, so W's lines do not displace the packed
+// operands the GEMM reads next from the Infinity Cache)
+template <int kAux = 0>
 __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                     float range, float *__restrict__ scale, int8_t *__restrict__ q,
                                                     int64_t k_pad, uint8_t *lds, float *red) {
@@ -803,13 +819,13 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
         for (int e = 0; e < 4; ++e)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 src, (lds_void *)(lds + ((i * 4 + e) * 16 + wv) * 1024), 16,
-                (int)(vrow + (uint32_t)((e + 512 * (i + kW32RegI)) * wsh * 4)), 0, 0, 0);
+                (int)(vrow + (uint32_t)((e + 512 * (i + kW32RegI)) * wsh * 4)), 0, 0, kAux);
     float4 v[kW32RegI][4];
 #pragma unroll
     for (int i = 0; i < kW32RegI; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 512 * i) * wsh * 4), 0, 0);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 512 * i) * wsh * 4), 0, kAux);
             v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
     float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
@@ -905,7 +921,7 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
 
 // kMap (block -> strip order; lab A/B): 0 = XCD-contiguous strip ranges, 1 = strip = block, 2 = even strips
 // first then odd, 3 = strips 4j, then 4j + 1, ... (the blocks on the chip at one time spread over the row)
-template <int kMap = 0>
+template <int kMap = 0, int kAux = 0>
 __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
@@ -938,7 +954,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
                 strip = (j * P + ph) * c + g;
             }
         }
-        pack_w_strip32_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
+        pack_w_strip32_body<kAux>(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kW32Cols;
         zero_packed_rows(w_q, n0, kW32Cols, k_pad, threadIdx.x, 1024);
