@@ -626,6 +626,11 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const float *__restrict_
 // split-K tickets).  Pass 1 is colmax_kernel alone: a clean sweep of W.  lab/c3d_lab.hip, FFN down, one box,
 // interleaved (profiles/r04_c3d_xrows.log): passes 97.3 + 63.5 -> 50.9 + 95.2 us, call 281.2 -> 267.5 us; the GEMM
 // after it unchanged (121.3 vs 120.3 us).
+// kNtW / kNtX: W's and X's fp32 loads non-temporal (the product sets both).  This pass is the last reader of them,
+// and with default loads their 384 MiB push the packed operands the GEMM reads next out of the Infinity Cache: the
+// FFN-down GEMM takes 108-110 us with its operands resident and 120-123 us after any 512-MiB sweep
+// (lab/c3g_lab.hip, profiles/r04_c3g_lab.log: non-temporal sweeps leave them resident, default or sc1 ones do not).
+// Call 264.9 -> 248.3 us: pass 2 94.2 -> 87.3, GEMM 120.8 -> 109.4 (profiles/r04_c3d_nt.log).
 template <bool kNtW = false, bool kNtX = false>
 __global__ __launch_bounds__(256) void pack_cols_then_rows_kernel(
     const float *__restrict__ w, int64_t wsh, int k, int n, float range, const uint32_t *__restrict__ partial,
@@ -1342,7 +1347,8 @@ hipError_t launch_pack_two_pass(const float *a, int64_t ash, int m, int k, Packe
                                 int n, PackedView outb, float range, hipStream_t stream, uint32_t *zero_words, int nzero) {
     if (k < 2 || !rows_vec_ok(a, ash, 1, m) || !cols_vec_ok(b, bsh, n)) return hipErrorNotSupported;
     if (rows_regs(k) < 0) {
-        // long rows: W-only pass 1 (column maxima), then pass 2 bottom-up with X's rows at its end
+        // long rows: W-only pass 1 (column maxima), then pass 2 bottom-up with X's rows at its end, both read
+        // non-temporally (they would displace the packed operands from the Infinity Cache)
         const int col_blocks = (n + kColBlock - 1) / kColBlock;
         colmax_kernel<true><<<dim3((unsigned)col_blocks, (unsigned)outb.parts), 256, 0, stream>>>(b, bsh, k, n, outb.scratch,
                                                                                                outb.rows_pad);
@@ -1350,7 +1356,7 @@ hipError_t launch_pack_two_pass(const float *a, int64_t ash, int m, int k, Packe
         if (e != hipSuccess) return e;
         const unsigned gx = (unsigned)(outb.rows_pad / kTc);
         const unsigned gy = (unsigned)((outb.k_pad / kTk + kTilesPerBlock - 1) / kTilesPerBlock);
-        pack_cols_then_rows_kernel<<<gx * gy + (unsigned)outa.rows_pad, 256, 0, stream>>>(
+        pack_cols_then_rows_kernel<true, true><<<gx * gy + (unsigned)outa.rows_pad, 256, 0, stream>>>(
             b, bsh, k, n, range, outb.scratch, outb.parts, outb.rows_pad, outb.scale, outb.q, outb.k_pad, (int)gx, (int)gy,
             a, ash, m, outa.scale, outa.q, outa.rows_pad, zero_words, nzero);
         return hipGetLastError();
