@@ -144,7 +144,7 @@ __device__ __forceinline__ bool om_bit(const OutlierMask &om, int k) { return (o
 // R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
 // kStage: the packed row goes to `stage` (the wave's LDS row, dword c at stage[c]) instead of q; the caller
 // writes the block's staged rows out as whole 128-B lines of the fragment-major q (write_staged_rows).
-template <int R, bool kMask = false, bool kWT = false, bool kStage = false>
+template <int R, bool kMask = false, bool kWT = false, bool kStage = false, int kAux = 0>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
@@ -191,7 +191,7 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, 0);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, kAux);
             v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
         if constexpr (kMask) {
@@ -991,7 +991,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
 // n = 8192 at K >= 2048, worse for wider W (n = 12288, 16384) and short K, where the 16-column pass stays.
 constexpr int kWs8Cols = 8;
 
-template <bool kMask = false, bool kWT = false>
+template <bool kMask = false, bool kWT = false, int kAux = 0>
 __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                    float range, float *__restrict__ scale, int8_t *__restrict__ q,
                                                    int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */,
@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, 0);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, kAux);
             v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
     bool seed_masked = false;
@@ -1121,7 +1121,8 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
 
 // Roles by block id: [W strips][W padding][X rows] (measured against W / X alternating and X rows first:
 // 29.1 vs 35.6 / 30.5 µs at 4096^3, 41.0 vs 42.2 / 43.0 at 8192 x 4096^2; profiles/r03_pack8_order_lab.log)
-template <int kWavesPerEu, bool kMask = false>
+// kWAux / kXAux: cache-policy bits of W's / X's loads (2 = non-temporal; lab)
+template <int kWavesPerEu, bool kMask = false, int kWAux = 0, int kXAux = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu, kWavesPerEu))) void pack_single_pass8_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
@@ -1136,7 +1137,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         // blocks b, b+8, ... run on one XCD: XCD-contiguous strip ranges (bijective for any nstrips)
         const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
         const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-        pack_w_strip8_body<kMask>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
+        pack_w_strip8_body<kMask, false, kWAux>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kWs8Cols;
         zero_packed_rows(w_q, n0, kWs8Cols, k_pad, threadIdx.x, 512);
@@ -1146,8 +1147,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         // 128-B lines of the fragment-major q (a line = 8 rows x 16 B: exactly this block's rows)
         const int64_t xb = bid - nstrips - npad;
         const int rsw = (int)(k_pad >> 2) + 16;
-        pack_rows_vec_body<16, kMask, false, true>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om,
-                                                   xstage + (threadIdx.x >> 6) * rsw);
+        pack_rows_vec_body<16, kMask, false, true, kXAux>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad,
+                                                          &om, xstage + (threadIdx.x >> 6) * rsw);
         __syncthreads();
         write_staged_rows<8>(xstage, rsw, x_q, xb * 8, k_pad);
     }
