@@ -3,8 +3,11 @@
 // W 64 MiB in, 48 MiB packed, 128 MiB of C: more than the 256-MB Infinity Cache holds, so the inputs are not found
 // again by the next call anyway and default loads may only push the packed operands out before the GEMM reads them
 // (lab/c3g_lab.hip: the FFN-down GEMM ran 11 % slower with its operands evicted).  At C2 (224 MiB per call) the
-// inputs do stay resident between calls, so non-temporal loads should cost there.  Steady-state calls, events
-// around each kernel, interleaved rounds; every variant's output compared with the default's.
+// inputs do stay resident between calls, so non-temporal loads should cost there (measured: they do, and the
+// GEMM does not move; profiles/r04_c4_lab_*.log, with a staggered-first-wave GEMM that did not pay either).  Now
+// also the packed outputs' store policy: non-temporal or write-through stores leave fewer dirty L2 lines to write
+// back at the pack's end.  Steady-state calls, events around each kernel, interleaved rounds; every variant's
+// output compared with the default's.
 //   build/c4_lab [m n k rounds]
 #include <cstdio>
 #include <cstdlib>
@@ -31,15 +34,21 @@ int main(int argc, char **argv) {
     hipStream_t s0; CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
     const int nstrips = n / kWs8Cols, npad = (int)((vw.rows_pad - n) / kWs8Cols), nx = (int)(vx.rows_pad / 8);
     const int g = nstrips + npad + nx;
-#define QG_P8(WA, XA)                                                                                              \
-    pack_single_pass8_kernel<5, false, WA, XA><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, \
+#define QG_P8(WA, XA, WS, XS)                                                                                      \
+    pack_single_pass8_kernel<5, false, WA, XA, WS, XS><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, \
                                                                  W, n, n, vw.scale, vw.q, vw.rows_pad, nstrips,    \
                                                                  127.f, nullptr, 0)
+    // variants: 0 default; 1-3 non-temporal loads (X / W / both, round 4: rejected); 4 packed W stored nt, 5 packed
+    // X stored nt, 6 both nt, 7 packed W stored sc1 (write-through): fewer dirty L2 lines at the pack's end
     auto pack = [&](int v) {
-        if (v == 0) QG_P8(0, 0);
-        if (v == 1) QG_P8(0, 2);
-        if (v == 2) QG_P8(2, 0);
-        if (v == 3) QG_P8(2, 2);
+        if (v == 0) QG_P8(0, 0, 0, false);
+        if (v == 1) QG_P8(0, 2, 0, false);
+        if (v == 2) QG_P8(2, 0, 0, false);
+        if (v == 3) QG_P8(2, 2, 0, false);
+        if (v == 4) QG_P8(0, 0, 2, false);
+        if (v == 5) QG_P8(0, 0, 0, true);
+        if (v == 6) QG_P8(0, 0, 2, true);
+        if (v == 7) QG_P8(0, 0, 16, false);
     };
     const int tiles_m = m / 256, tiles_n = n / 256;
     auto gemm = [&](int stagger = 0) {
@@ -52,15 +61,14 @@ int main(int argc, char **argv) {
         if (stagger == 2) gemm_i8_fm<kEpiNone, false, kSplitNone, true, 30, false, 2><<<tiles_m * tiles_n, 256, 0, s0>>>(p);
         if (stagger == 3) gemm_i8_fm<kEpiNone, false, kSplitNone, true, 30, false, 3><<<tiles_m * tiles_n, 256, 0, s0>>>(p);
     };
-    // modes 0-3: pack variant + GEMM; 4: GEMM back to back; 5-7: GEMM back to back, half the first-wave blocks
-    // delayed 1 / 2 / 3 x ~4 us (kStagger); 8: default pack + GEMM with stagger 2
+    // modes: pack variant v (0..7) + GEMM; 8: GEMM back to back
     constexpr int kModes = 9;
-    const char *names[kModes] = {"default", "nt_x", "nt_w", "nt_w_x", "gemm_b2b", "b2b_stag1", "b2b_stag2", "b2b_stag3",
-                                 "call_stag2"};
+    const char *names[kModes] = {"default", "nt_x", "nt_w", "nt_w_x", "st_nt_w", "st_nt_x", "st_nt_wx", "st_sc1_w",
+                                 "gemm_b2b"};
     std::vector<float> ref((size_t)m * n), got(ref.size());
     pack(0); gemm(); CK(hipStreamSynchronize(s0)); CK(hipGetLastError());
     CK(hipMemcpy(ref.data(), C, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int v = 1; v < 4; ++v) {
+    for (int v = 1; v < 8; ++v) {
         CK(hipMemsetAsync(PW, 0x5a, packed_bytes(n, k), s0)); CK(hipMemsetAsync(PX, 0x5a, packed_bytes(m, k), s0));
         CK(hipMemsetAsync(C, 0xff, (size_t)m * n * 4, s0));
         pack(v); gemm(); CK(hipStreamSynchronize(s0)); CK(hipGetLastError());
@@ -70,21 +78,14 @@ int main(int argc, char **argv) {
     hipEvent_t ev[3];
     for (auto &e : ev) CK(hipEventCreate(&e));
     for (int i = 0; i < 200; ++i) { pack(0); gemm(); }  // clocks up
-    for (int st = 1; st <= 3; ++st) {  // the staggered GEMM writes the same bytes
-        CK(hipMemsetAsync(C, 0xff, (size_t)m * n * 4, s0));
-        gemm(st); CK(hipStreamSynchronize(s0)); CK(hipGetLastError());
-        CK(hipMemcpy(got.data(), C, got.size() * 4, hipMemcpyDeviceToHost));
-        printf("check stagger %d %s\n", st, memcmp(ref.data(), got.data(), ref.size() * 4) ? "DIFF" : "same");
-    }
     std::vector<float> tp[kModes], tg[kModes];
     for (int r = 0; r < rounds; ++r)
         for (int md = 0; md < kModes; ++md) {
             float ap = 0, ag = 0;
             for (int j = 0; j < reps + 3; ++j) {
                 CK(hipEventRecord(ev[0], s0));
-                if (md < 4) pack(md);
-                if (md == 8) pack(0);
-                CK(hipEventRecord(ev[1], s0)); gemm(md >= 5 && md <= 7 ? md - 4 : md == 8 ? 2 : 0);
+                if (md < 8) pack(md);
+                CK(hipEventRecord(ev[1], s0)); gemm();
                 CK(hipEventRecord(ev[2], s0)); CK(hipEventSynchronize(ev[2]));
                 float x;
                 if (j < 3) continue;
