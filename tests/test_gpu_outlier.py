@@ -51,6 +51,18 @@ def test_outlier_fast_path_bit_exact(qg, oracle, device, M, N, K, cols):
     assert_bits_equal(C.cpu().numpy(), want, f"outlier fast path {M}x{N}x{K}")
 
 
+# the fast path at 128 and 129 flag chunks of 64 rows (the index launch ORs every chunk word; a round-4 variant that
+# folded that OR into the pack below 129 chunks, lab/outlier_fold_experiment.patch, was tested here), counts read
+# back from the workspace
+@pytest.mark.parametrize("M,N,K,cols", [(8192, 1280, 128, [0, 31, 32, 127]), (8256, 1280, 256, [1, 64, 200, 255])])
+def test_outlier_fast_path_many_chunks(qg, oracle, device, M, N, K, cols):
+    X, W = _with_outliers(oracle, M, N, K, cols, 13)
+    C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    assert cnt == wcnt == len(cols)
+    assert_bits_equal(C.cpu().numpy(), want, f"outlier fast path {M}x{N}x{K}")
+
+
 def test_outlier_fast_path_nan_and_none(qg, oracle, device):
     X, W = oracle.inputs(2560, 4096, 128, 10)
     C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
