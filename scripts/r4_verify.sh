@@ -1,0 +1,14 @@
+#!/bin/bash
+# round-4 closing check of the committed tree: the GPU suite, smoke, the default bench line, c3_down
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r4verify; mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { tail -30 $out/pytest.log; exit 1; }
+tail -2 $out/pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail $out/smoke.log; exit 1; }
+tail -1 $out/smoke.log
+timeout -k 10 300 python bench.py > $out/bench_c2.log 2>&1 || exit 1
+grep -o '"value": [0-9.]*' $out/bench_c2.log | head -1
+timeout -k 10 300 python bench.py --config c3_down --no-cpu-baseline > $out/bench_c3_down.log 2>&1 || exit 1
+grep -o '"value": [0-9.]*' $out/bench_c3_down.log | head -1
+echo done
