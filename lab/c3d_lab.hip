@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
         if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);
     };
     struct V { std::string name; int order; int g; };
-    std::vector<V> vs = {{"product", 2, 2}, {"nt_w_x", 3, 2}, {"nt_x", 4, 2}};
+    std::vector<V> vs = {{"wonly_default", 2, 2}, {"product_nt", 3, 2}, {"nt_fk", 3, 3}, {"nt_both_slabs", 3, 0}};
     // reference: the library's order
     pass1(0); pass2(0); gemm(0, Cref);
     CK(hipStreamSynchronize(s0));
@@ -111,7 +111,7 @@ int main(int argc, char **argv) {
     hipEvent_t ev[4];
     for (auto &e : ev) CK(hipEventCreate(&e));
     std::vector<std::vector<float>> tc(vs.size()), t1(vs.size()), t2(vs.size()), tg(vs.size());
-    for (int i = 0; i < 300; ++i) { pass1(2); pass2(2); gemm(2, C); }  // clocks up
+    for (int i = 0; i < 300; ++i) { pass1(3); pass2(3); gemm(2, C); }  // clocks up
     for (int r = 0; r < rounds; ++r)
         for (size_t i = 0; i < vs.size(); ++i) {
             const V &v = vs[i];
