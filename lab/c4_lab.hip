@@ -9,6 +9,8 @@
 // back at the pack's end.  Steady-state calls, events around each kernel, interleaved rounds; every variant's
 // output compared with the default's.
 //   build/c4_lab [m n k rounds]
+// Needs the rejected knobs: `git apply lab/cache_policy_knobs_experiment.patch` (csrc/pack.hip, gemm_i8_kernels.h)
+// before building, `git apply -R` after.
 #include <cstdio>
 #include <cstdlib>
 #include <vector>

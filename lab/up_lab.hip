@@ -11,6 +11,8 @@
 // times the whole FFN-up call (pack + gemm_i8_fm with row rotation), the pack's W loads default vs non-temporal:
 // does the GEMM run faster when W's fp32 lines have not displaced the packed operands from the Infinity Cache?
 //   build/up_lab [m n k rounds]
+// Needs the rejected knobs: `git apply lab/cache_policy_knobs_experiment.patch` (csrc/pack.hip, gemm_i8_kernels.h)
+// before building, `git apply -R` after.
 #include <cstdio>
 #include <cstdlib>
 #include <vector>

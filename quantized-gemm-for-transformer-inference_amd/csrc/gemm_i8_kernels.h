@@ -215,10 +215,8 @@ enum SplitMode { kSplitNone = 0, kSplitBoth = 1, kSplitFirst = 2 };
 // 58.2 vs 59.5 us by events; profiles/r03_ab_nt_c.log) -- the 64-MiB tail streams past the caches
 // kPairXcd (kSplitFirst only): blocks b and b + 8 share an XCD; XCD 2j takes K slice 0 and XCD 2j + 1 slice 1 of the
 // same 32 tiles (a 4 x 8 patch), so each XCD fetches 4 A + 8 B half-panels instead of 4 + 4 whole panels
-// kStagger (lab): half of the first 256 blocks (every other group of 8: half the CUs of every XCD) sleep kStagger x
-// ~4 us before they start, so that on 2-tiles-per-CU plans the two halves' store tails fall at different times
 template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30,
-          bool kPairXcd = false, int kStagger = 0>
+          bool kPairXcd = false>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
@@ -226,10 +224,6 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     constexpr int TS = 132;                 // padded row of a wave's epilogue block (conflict-free ds_write)
     constexpr int kBlockBytes = 64 * TS * 4;
     __shared__ __attribute__((aligned(16))) int8_t lds[4 * kBlockBytes + 2048 + 16];
-    if constexpr (kStagger > 0) {
-        if (blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
-            for (int i = 0; i < kStagger; ++i) __builtin_amdgcn_s_sleep(127);
-    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;

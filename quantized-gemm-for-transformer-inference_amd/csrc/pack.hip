@@ -144,7 +144,7 @@ __device__ __forceinline__ bool om_bit(const OutlierMask &om, int k) { return (o
 // R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
 // kStage: the packed row goes to `stage` (the wave's LDS row, dword c at stage[c]) instead of q; the caller
 // writes the block's staged rows out as whole 128-B lines of the fragment-major q (write_staged_rows).
-template <int R, bool kMask = false, bool kWT = false, bool kStage = false, int kAux = 0>
+template <int R, bool kMask = false, bool kWT = false, bool kStage = false>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
@@ -191,7 +191,7 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, kAux);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, 0);
             v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
         if constexpr (kMask) {
@@ -279,7 +279,7 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
 // lane groups for k_pad / 4 = 0 or 32 mod 64; + 8 left 2-way conflicts, 6.5 % of the pack's LDS cycles), written out as whole 128-B lines of the fragment-major q: line (L, h) = the 16-B pieces
 // of k 16L .. 16L+15 of rows 8h .. 8h+7; one wave store instruction = 8 lines.  After a block barrier.
 constexpr int kStageRowWordsMax = 4096 / 4 + 16;
-template <int kRows, bool kNtStore = false>
+template <int kRows>
 __device__ __forceinline__ void write_staged_rows(const uint32_t *stage, int rsw, int8_t *__restrict__ q, int64_t row0,
                                                   int64_t k_pad) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -289,13 +289,7 @@ __device__ __forceinline__ void write_staged_rows(const uint32_t *stage, int rsw
         const int h = u / nl, L = u - h * nl;
         const int r = h * 8 + (lane & 7);
         const uint4 v = *reinterpret_cast<const uint4 *>(stage + r * rsw + 4 * L);
-        if constexpr (kNtStore) {
-            typedef unsigned v4u_nt __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(v4u_nt{v.x, v.y, v.z, v.w},
-                                        reinterpret_cast<v4u_nt *>(q + fofs(row0 + r, 16 * L, k_pad)));
-        } else {
-            *reinterpret_cast<uint4 *>(q + fofs(row0 + r, 16 * L, k_pad)) = v;
-        }
+        *reinterpret_cast<uint4 *>(q + fofs(row0 + r, 16 * L, k_pad)) = v;
     }
 }
 
@@ -810,9 +804,6 @@ constexpr int kW32LdsBytes = kW32LdsI * 4 * 16 * 1024;  // [i][e][wave] x 1 KiB
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// kAux: cache-policy bits of W's loads (0: default; 2: non-temporal, so W's lines do not displace the packed
-// operands the GEMM reads next from the Infinity Cache)
-template <int kAux = 0>
 __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                     float range, float *__restrict__ scale, int8_t *__restrict__ q,
                                                     int64_t k_pad, uint8_t *lds, float *red) {
@@ -830,13 +821,13 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
         for (int e = 0; e < 4; ++e)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 src, (lds_void *)(lds + ((i * 4 + e) * 16 + wv) * 1024), 16,
-                (int)(vrow + (uint32_t)((e + 512 * (i + kW32RegI)) * wsh * 4)), 0, 0, kAux);
+                (int)(vrow + (uint32_t)((e + 512 * (i + kW32RegI)) * wsh * 4)), 0, 0, 0);
     float4 v[kW32RegI][4];
 #pragma unroll
     for (int i = 0; i < kW32RegI; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 512 * i) * wsh * 4), 0, kAux);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 512 * i) * wsh * 4), 0, 0);
             v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
     float p0 = -INFINITY, p1 = -INFINITY, p2 = -INFINITY, p3 = -INFINITY;
@@ -932,7 +923,7 @@ __device__ __forceinline__ void pack_w_strip32_body(int strip, const float *__re
 
 // kMap (block -> strip order; lab A/B): 0 = XCD-contiguous strip ranges, 1 = strip = block, 2 = even strips
 // first then odd, 3 = strips 4j, then 4j + 1, ... (the blocks on the chip at one time spread over the row)
-template <int kMap = 0, int kAux = 0>
+template <int kMap = 0>
 __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
@@ -965,7 +956,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
                 strip = (j * P + ph) * c + g;
             }
         }
-        pack_w_strip32_body<kAux>(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
+        pack_w_strip32_body(strip, w, wsh, k, range, w_scale, w_q, k_pad, lds_w, red);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kW32Cols;
         zero_packed_rows(w_q, n0, kW32Cols, k_pad, threadIdx.x, 1024);
@@ -997,7 +988,7 @@ __global__ __launch_bounds__(1024) void pack_single_pass32_kernel(
 // n = 8192 at K >= 2048, worse for wider W (n = 12288, 16384) and short K, where the 16-column pass stays.
 constexpr int kWs8Cols = 8;
 
-template <bool kMask = false, bool kWT = false, int kAux = 0, int kStAux = 0>
+template <bool kMask = false, bool kWT = false>
 __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__restrict__ w, int64_t wsh, int k,
                                                    float range, float *__restrict__ scale, int8_t *__restrict__ q,
                                                    int64_t k_pad, float *red /* [8 waves][8 cols] + [8] */,
@@ -1027,7 +1018,7 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, kAux);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, 0);
             v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
     bool seed_masked = false;
@@ -1120,17 +1111,14 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
         if (kp < k_pad) {
             typedef int v4i_t __attribute__((ext_vector_type(4)));
             const v4i_t val = {(int)pc[0], (int)pc[1], (int)pc[2], (int)pc[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(val, dst, (uint32_t)fofs(prow, kp, k_pad), 0,
-                                                   kWT ? 16 /* sc1 */ : kStAux);
+            __builtin_amdgcn_raw_buffer_store_b128(val, dst, (uint32_t)fofs(prow, kp, k_pad), 0, kWT ? 16 /* sc1 */ : 0);
         }
     }
 }
 
 // Roles by block id: [W strips][W padding][X rows] (measured against W / X alternating and X rows first:
 // 29.1 vs 35.6 / 30.5 µs at 4096^3, 41.0 vs 42.2 / 43.0 at 8192 x 4096^2; profiles/r03_pack8_order_lab.log)
-// kWAux / kXAux: cache-policy bits of W's / X's loads (2 = non-temporal; lab); kWStAux: of the packed W stores;
-// kXNtSt: the packed X rows stored non-temporally (lab)
-template <int kWavesPerEu, bool kMask = false, int kWAux = 0, int kXAux = 0, int kWStAux = 0, bool kXNtSt = false>
+template <int kWavesPerEu, bool kMask = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu, kWavesPerEu))) void pack_single_pass8_kernel(
     const float *__restrict__ x, int64_t xsh, int m, int k, float *__restrict__ x_scale, int8_t *__restrict__ x_q,
     int64_t x_rows_pad, int64_t k_pad, const float *__restrict__ w, int64_t wsh, int n, float *__restrict__ w_scale,
@@ -1145,7 +1133,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         // blocks b, b+8, ... run on one XCD: XCD-contiguous strip ranges (bijective for any nstrips)
         const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
         const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-        pack_w_strip8_body<kMask, false, kWAux, kWStAux>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
+        pack_w_strip8_body<kMask>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kWs8Cols;
         zero_packed_rows(w_q, n0, kWs8Cols, k_pad, threadIdx.x, 512);
@@ -1155,10 +1143,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         // 128-B lines of the fragment-major q (a line = 8 rows x 16 B: exactly this block's rows)
         const int64_t xb = bid - nstrips - npad;
         const int rsw = (int)(k_pad >> 2) + 16;
-        pack_rows_vec_body<16, kMask, false, true, kXAux>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad,
-                                                          &om, xstage + (threadIdx.x >> 6) * rsw);
+        pack_rows_vec_body<16, kMask, false, true>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om,
+                                                   xstage + (threadIdx.x >> 6) * rsw);
         __syncthreads();
-        write_staged_rows<8, kXNtSt>(xstage, rsw, x_q, xb * 8, k_pad);
+        write_staged_rows<8>(xstage, rsw, x_q, xb * 8, k_pad);
     }
 }
 
