@@ -5,11 +5,16 @@ One "step" = one full drop-in call on inputs already resident in HBM: pack X (Cx
 (Cw + W_int8^T), int8 MFMA GEMM with the fused dequantize epilogue -- exactly the reference's
 op_quantized_mm chain (op_mm.cuh:67-101), which re-quantizes both operands every call.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched under
-torch.distributed.run, one rank per GPU.  Each rank owns its own M-shard (weak scaling over batched
-M: every rank runs the BASELINE configs[1] problem, M=N=K=4096, on its own rows with the replicated
-W); no data-path collective.  Timed region: barrier + synchronize, K steps, synchronize + barrier,
-max over ranks.  Rank 0 prints ONE JSON line.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the driver launches it
+under torch.distributed.run, one rank per GPU.  Run WITHOUT a launcher (no WORLD_SIZE in the environment)
+and N > 1, bench.py launches itself that way: ``python -m torch.distributed.run --nnodes=1
+--nproc-per-node N --master-addr 127.0.0.1 ...`` as a CHILD process, before importing torch or touching
+the GPU, and exits with the child's code (rank 0's JSON line reaches the same stdout).  A WORLD_SIZE that
+differs from --gpus is an error (exit 2): n_gpus always equals --gpus, and `rccl_world` is the size RCCL
+itself reports for the product's communicator (ncclCommCount).  Each rank owns its own M-shard (weak
+scaling over batched M: every rank runs the BASELINE configs[1] problem, M=N=K=4096, on its own rows
+with the replicated W); no data-path collective.  Timed region: barrier + synchronize, K steps,
+synchronize + barrier, max over ranks.  Rank 0 prints ONE JSON line.
 
 Extra objects on that line:
   roofline     -- the dominant kernel (the int8 GEMM): algorithmic 2*M*N*K int8 ops per launch over
@@ -26,6 +31,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -64,7 +71,7 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
@@ -88,7 +95,42 @@ def parse():
                    help="how the GEMM kernel is timed inside the timed region: hipExtLaunchKernel start/stop "
                         "events (ext, exact kernel bounds), hipEventRecord around its launch (record, includes the "
                         "kernel-boundary gap), or not at all (none)")
-    return p.parse_args()
+    p.add_argument("--node-chunks", type=int, default=0,
+                   help="row chunks per rank of the pipelined whole-node C4 step (0 = rows / 4096, at least 1)")
+    p.add_argument("--launch-dry-run", action="store_true",
+                   help="N > 1 without WORLD_SIZE: print the child launcher command as JSON instead of running it")
+    return p.parse_args(argv)
+
+
+def world_mode(args, env):
+    """How this process runs: ("launch", None) -- N > 1 and no launcher: start torch.distributed.run as a
+    child; ("run", world) -- run the ranks' body here; ("error", message) -- WORLD_SIZE disagrees with
+    --gpus (the driver would otherwise read a 1-rank line as an N-GPU one)."""
+    if args.gpus < 1:
+        return "error", f"--gpus must be >= 1, got {args.gpus}"
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", None) if args.gpus > 1 else ("run", 1)
+    try:
+        world = int(ws)
+    except ValueError:
+        return "error", f"WORLD_SIZE={ws!r} is not an integer"
+    if world != args.gpus:
+        return "error", f"WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU (torch.distributed.run " \
+                        f"--nproc-per-node {args.gpus}) or pass --gpus {world}"
+    return "run", world
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(args, argv, port):
+    """The child command for N ranks on this node (the driver's own form of the launch)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
 class HipEvents:
@@ -138,6 +180,7 @@ def load_pkg():
     import _pkg
     qg = _pkg.package(build=False)
     qg.load()  # raises if the HIP library is missing: no fallback
+    qg.check_binary()  # raises if build/ was compiled from other sources than this tree's
     return qg
 
 
@@ -283,23 +326,36 @@ def node_phase_times(reps, warm, distributed, run_step, dev):
     return comp, gath
 
 
-def c4_node(args, qg, dev, world, rank, distributed):
+def c4_node(args, qg, dev, world, rank, distributed, comm):
     """BASELINE configs[3] as a whole-node figure: the global M = 65536 x 4096 x 4096 problem with M sharded
     over the `world` ranks (op_mm_quantize_shard: per-rank pointer offsets into the full A and C), then the
     in-place RCCL all-gather of C over xGMI (qgemm_allgather_rows, libqgemm_dist.so -- our own rccl.h call
-    site; the communicator's id travels over torch.distributed).  Warm: 2 untimed steps, then
-    args.node_reps steps, each bracketed by a barrier; per step the max over ranks of each phase, reported
-    as medians.  Kept OUT of `value` (the gather moves 1 GiB of C, ~10x the compute)."""
+    site on `comm`, the product communicator).  Warm: 2 untimed steps, then args.node_reps steps, each
+    bracketed by a barrier; per step the max over ranks of each phase, reported as medians.  Then the
+    PIPELINED step (op_mm_quantize_shard_pipelined): W packed once, the rank's rows in chunks, chunk c's
+    broadcasts on a second stream under chunk c + 1's compute; its whole time per step, max over ranks.
+    Kept OUT of `value` (the gather moves 1 GiB of C, ~10x the compute)."""
     import statistics
     import torch
-    import torch.distributed as dist
     Mg, N, K = 65536, 4096, 4096
     A = qg.fill_uniform(torch.empty((Mg, K), device=dev), seed=2 * 7)  # the same A on every rank
     B = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 7 + 1)
     C = torch.empty((Mg, N), device=dev)
-    uid = share_comm_id(rank, distributed, qg.Comm.unique_id, qg.COMM_ID_BYTES)
-    comm = qg.Comm(world, rank, uid)
+    m0, rows = qg.shard_rows(Mg, world, rank)
+    chunks = args.node_chunks if args.node_chunks > 0 else max(1, rows // 4096)
     hip = HipEvents(3)
+    gstream = torch.cuda.Stream(dev)
+    ws = torch.empty(qg.load_dist().op_mm_quantize_shard_pipelined_workspace_size(Mg, N, K, world, chunks),
+                     dtype=torch.uint8, device=dev)
+    probe = [qg.shard_rows(Mg, world, r)[0] for r in range(world)]
+    Cref = torch.empty((len(probe), N), device=dev)
+    for i, r0 in enumerate(probe):  # one row of every shard, by this rank's own one-GPU call
+        qg.op_mm_quantize(A[r0:r0 + 1].contiguous(), B, Cref[i:i + 1])
+
+    def gathered_ok():
+        torch.cuda.synchronize(dev)
+        return bool(torch.equal(C[probe].view(torch.int32), Cref.view(torch.int32)))
+
     try:
         def one_step():
             torch.cuda.synchronize(dev)
@@ -312,18 +368,23 @@ def c4_node(args, qg, dev, world, rank, distributed):
             return hip.elapsed_ms(hip.ev[0], hip.ev[1]), hip.elapsed_ms(hip.ev[1], hip.ev[2])
 
         comp, gath = node_phase_times(args.node_reps, 2, distributed, one_step, dev)
-        # every rank now holds the whole C: check one row of every shard against this rank's own call
-        m0, rows = qg.shard_rows(Mg, world, rank)
-        probe = [qg.shard_rows(Mg, world, r)[0] for r in range(world)]
-        Cref = torch.empty((len(probe), N), device=dev)
-        for i, r0 in enumerate(probe):
-            qg.op_mm_quantize(A[r0:r0 + 1].contiguous(), B, Cref[i:i + 1])
-        torch.cuda.synchronize(dev)
-        gathered_ok = bool(torch.equal(C[probe].view(torch.int32), Cref.view(torch.int32)))
+        serial_ok = gathered_ok()
+
+        def pipe_step():
+            torch.cuda.synchronize(dev)
+            s = qg._stream(dev)
+            hip.hip.hipEventRecord(hip.ev[0], s)
+            qg.op_mm_quantize_shard_pipelined(A, B, C, world, rank, chunks, comm=comm, gather_stream=gstream,
+                                              workspace=ws)
+            hip.hip.hipEventRecord(hip.ev[1], s)  # the call leaves s waiting for the last broadcast
+            return hip.elapsed_ms(hip.ev[0], hip.ev[1]), 0.0
+
+        C.fill_(float("nan"))
+        pipe, _ = node_phase_times(args.node_reps, 2, distributed, pipe_step, dev)
+        pipe_ok = gathered_ok()
     finally:
-        comm.close()
         hip.destroy()
-    cm, gm = statistics.median(comp), statistics.median(gath)
+    cm, gm, pm = statistics.median(comp), statistics.median(gath), statistics.median(pipe)
     return {
         "workload": f"BASELINE configs[3]: M={Mg} K=N={N} sharded over {world} GPU(s) ({Mg // world} rows each) + "
                     "in-place RCCL all-gather of C (1 GiB) over xGMI",
@@ -333,7 +394,14 @@ def c4_node(args, qg, dev, world, rank, distributed):
         "node_gemms_per_s_with_allgather": round(1e3 / (cm + gm), 2),
         "node_tops_compute": round(2.0 * Mg * N * K / (cm * 1e-3) / 1e12, 1),
         "allgather_GBps_recv_per_rank": round(Mg * N * 4 * (world - 1) / world / (gm * 1e-3) / 1e9, 1) if world > 1 else None,
-        "gathered_rows_match_one_gpu": gathered_ok,
+        "gathered_rows_match_one_gpu": serial_ok,
+        "pipelined": {
+            "chunks_per_rank": chunks, "ms_median": round(pm, 4),
+            "node_gemms_per_s_with_allgather": round(1e3 / pm, 2),
+            "gathered_rows_match_one_gpu": pipe_ok,
+            "note": "op_mm_quantize_shard_pipelined: W packed once, each chunk's rows quantized + GEMM on the "
+                    "compute stream, the chunk's per-owner in-place ncclBroadcasts on a second stream behind an "
+                    "event (under the next chunk's compute); serial = compute_ms + allgather_ms above"},
         "note": "the compute is a full drop-in call per rank on its row shard (pack + GEMM); world 1: the whole "
                 "65536-row problem on one GPU and a no-op gather",
     }
@@ -349,25 +417,137 @@ def gemm_kernel_name(L, M, N, K, outlier):
     return f"{name.value.decode()}, plan: {tile.value}-tiles x {splits} K-slice(s)"
 
 
-def main():
-    args = parse()
+def init_distributed(world, backend):
+    """This process's rank, local rank, whether it is one of several, and its device.  backend "nccl" (the
+    product run: RCCL, one GPU per rank) or "gloo" (the CPU tests of this branch)."""
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    if backend == "gloo":
+        if distributed:
+            dist.init_process_group("gloo")
+        return rank, local, distributed, torch.device("cpu")
     if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if distributed else 0)
     torch.cuda.set_device(dev)
+    return rank, local, distributed, dev
 
+
+def timed_region(step, steps, distributed, sync):
+    """The contract's timed region: barrier + synchronize, `steps` steps, synchronize + barrier; this rank's
+    wall seconds (the caller takes the max over ranks)."""
+    import torch.distributed as dist
+    if distributed:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    if distributed:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(vals, distributed, dev):
+    """Element-wise MAX of `vals` over the ranks (all_reduce); the values themselves at world 1."""
+    if not distributed:
+        return [float(v) for v in vals]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]
+
+
+def base_result(args, metric, unit, world, rccl_world, elapsed):
+    """The fields every line carries; value = all ranks' steps over the max-over-ranks time."""
+    return {
+        "metric": metric,
+        "value": round(world * args.steps / elapsed, 2),
+        "unit": unit,
+        "n_gpus": world,
+        "rccl_world": rccl_world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+    }
+
+
+METRIC = "int8 GEMMs/sec + achieved int8-MFMA TOPS%, M=N=K=4096, 1/2/4/8 MI355X"
+
+
+def main(argv=None, backend="nccl", stub_step=None):
+    """The contract's entry.  stub_step (tests only): run the ranks' body on `backend` with this CPU step in
+    place of the drop-in call -- the launch / world checks, timed region, max over ranks and the base line
+    are the product's own; nothing touches a GPU."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    mode, info = world_mode(args, os.environ)
+    if mode == "error":
+        print(f"bench.py: {info}", file=sys.stderr, flush=True)
+        return 2
+    if mode == "launch":
+        # N ranks and no launcher: torch.distributed.run as a CHILD (this process has not imported torch nor
+        # touched the GPU); rank 0's JSON line goes to the inherited stdout, the child's code is ours
+        cmd = launcher_command(args, argv, free_port())
+        if args.launch_dry_run:
+            print(json.dumps({"launch": cmd, "nproc": args.gpus}), flush=True)
+            return 0
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        return subprocess.call(cmd, env=env)
+    world = info
+    rank, local, distributed, dev = init_distributed(world, backend)
+    import torch.distributed as dist
+    try:
+        if stub_step is not None:
+            elapsed = timed_region(stub_step, args.steps, distributed, lambda: None)
+            (elapsed,) = max_over_ranks([elapsed], distributed, dev)
+            rw = dist.get_world_size() if distributed else 1
+            result = base_result(args, METRIC, "GEMMs/s", world, rw, elapsed)
+            result["backend"] = backend
+            if rank == 0:
+                print(json.dumps(result), flush=True)
+            return 0
+        return run_gpu(args, world, rank, distributed, dev)
+    finally:
+        if distributed:
+            dist.destroy_process_group()
+
+
+def product_comm(qg, world, rank, distributed):
+    """The product's RCCL communicator (libqgemm_dist.so) over every rank, its id shared through the
+    torch.distributed group; returns (comm, the size RCCL reports for it)."""
+    uid = share_comm_id(rank, distributed, qg.Comm.unique_id, qg.COMM_ID_BYTES)
+    comm = qg.Comm(world, rank, uid)
+    rw = comm.count()
+    if rw != world:
+        comm.close()
+        raise RuntimeError(f"RCCL communicator has {rw} ranks, expected {world}")
+    return comm, rw
+
+
+def run_gpu(args, world, rank, distributed, dev):
     qg = load_pkg()
     L = qg.load()
-    if args.config == "c5_encoder":
-        return bench_encoder(args, qg, L, dev, world, rank, distributed)
+    comm, rccl_world = product_comm(qg, world, rank, distributed)
+    try:
+        if args.config == "c5_encoder":
+            return bench_encoder(args, qg, L, dev, world, rank, distributed, rccl_world)
+        return bench_gemm(args, qg, L, dev, world, rank, distributed, comm, rccl_world)
+    finally:
+        comm.close()
+
+
+def bench_gemm(args, qg, L, dev, world, rank, distributed, comm, rccl_world):
+    import torch
     M, N, K, desc = CONFIGS[args.config]
 
     # inputs resident in HBM before timing; X differs per rank (its M-shard), W is replicated
@@ -419,43 +599,20 @@ def main():
     for _ in range(args.warmup):
         step()
 
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(step, args.steps, distributed, lambda: torch.cuda.synchronize(dev))
 
     if mode != "none":
         gemm_ms = sum(hip.elapsed_ms(hip.ev[2 * i], hip.ev[2 * i + 1]) for i in timed) / len(timed)
     else:
         gemm_ms = float("nan")
     hip.destroy()
-    if distributed:
-        t = torch.tensor([elapsed, gemm_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gemm_ms = float(t[0]), float(t[1])
+    elapsed, gemm_ms = max_over_ranks([elapsed, gemm_ms], distributed, dev)
 
     ops = 2.0 * M * N * K
     traffic, traffic_src = pmc_traffic(args.config)
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = world * args.steps / elapsed
     achieved = ops / (gemm_ms * 1e-3) / 1e12
-    result = {
-        "metric": "int8 GEMMs/sec + achieved int8-MFMA TOPS%, M=N=K=4096, 1/2/4/8 MI355X",
-        "value": round(value, 2),
-        "unit": "GEMMs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
+    result = base_result(args, METRIC, "GEMMs/s", world, rccl_world, elapsed)
+    result.update({
         "dtype": "int8",
         "data": "synthetic U(-1,1) fp32 inputs (seeded counter-based generator, generated in HBM)",
         "config": {
@@ -493,9 +650,9 @@ def main():
         },
         "library": qg.version(),
         "prewarm": prewarm,
-    }
+    })
     if args.config == "c2" and args.node_reps > 0:
-        node = c4_node(args, qg, dev, world, rank, distributed)
+        node = c4_node(args, qg, dev, world, rank, distributed, comm)
         result["c4_node"] = node
         result["allgather_ms_median"] = node["allgather_ms_median"]
     if rank == 0 and args.cold_steps > 0:
@@ -538,15 +695,13 @@ def main():
         result["config"]["outlier_columns"] = cnt
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if distributed:
-        dist.destroy_process_group()
+    return 0
 
 
-def bench_encoder(args, qg, L, dev, world, rank, distributed):
+def bench_encoder(args, qg, L, dev, world, rank, distributed, rccl_world):
     """BASELINE config 5: the encoder counterpart's forward (seeded weights packed once, the
     activations' quantize inside every forward); one forward per step, each rank its own sequence."""
     import torch
-    import torch.distributed as dist
     seq, d, H, dff, blocks, desc = CONFIGS["c5_encoder"]
     enc = qg.Encoder(d, H, dff, blocks, max_seq=seq, seed=1000)
     X = qg.fill_uniform(torch.empty((seq, d), device=dev), seed=2 * (1000 + rank))
@@ -558,39 +713,22 @@ def bench_encoder(args, qg, L, dev, world, rank, distributed):
     prewarm = prewarm_device(args, lambda: enc.forward(X, Y), dev)
     for _ in range(args.warmup):
         enc.forward(X, Y)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+
+    def step(i):
         if i % every == 0:  # times the forward's first GEMM: the fused Q/K/V projection
             L.qgemm_set_gemm_events(hip.ev[2 * i], hip.ev[2 * i + 1])
         enc.forward(X, Y)
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+
+    elapsed = timed_region(step, args.steps, distributed, lambda: torch.cuda.synchronize(dev))
     gemm_ms = sum(hip.elapsed_ms(hip.ev[2 * i], hip.ev[2 * i + 1]) for i in timed) / len(timed)
     hip.destroy()
-    if distributed:
-        t = torch.tensor([elapsed, gemm_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gemm_ms = float(t[0]), float(t[1])
+    elapsed, gemm_ms = max_over_ranks([elapsed, gemm_ms], distributed, dev)
     qkv_ops = 2.0 * seq * 3 * d * d
     lin_ops = blocks * 2.0 * seq * (3 * d * d + d * d + 2 * d * dff)
     attn_flops = blocks * 2.0 * 2 * H * seq * seq * (d // H)
     achieved = qkv_ops / (gemm_ms * 1e-3) / 1e12
-    result = {
-        "metric": "encoder forwards/s (BASELINE configs[4])",
-        "value": round(world * args.steps / elapsed, 2),
-        "unit": "forwards/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
+    result = base_result(args, "encoder forwards/s (BASELINE configs[4])", "forwards/s", world, rccl_world, elapsed)
+    result.update({
         "dtype": "int8",
         "data": "synthetic U(-1,1) fp32 input, seeded weights (qgemm_fill_uniform streams)",
         "config": {"workload": desc, "seq": seq, "d_model": d, "n_heads": H, "d_ff": dff, "n_blocks": blocks,
@@ -610,7 +748,7 @@ def bench_encoder(args, qg, L, dev, world, rank, distributed):
         },
         "library": qg.version(),
         "prewarm": prewarm,
-    }
+    })
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
         O.build()
@@ -633,9 +771,8 @@ def bench_encoder(args, qg, L, dev, world, rank, distributed):
     if rank == 0:
         print(json.dumps(result), flush=True)
     enc.close()
-    if distributed:
-        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -47,6 +47,10 @@ QGEMM_API int qgemm_comm_unique_id(void *id_out /* QGEMM_COMM_ID_BYTES */);
 QGEMM_API int qgemm_comm_init_rank(void **comm, int world, const void *id, int rank);
 QGEMM_API int qgemm_comm_init_all(void **comms, int ndev, const int *devices);
 QGEMM_API int qgemm_comm_destroy(void *comm);
+/* The communicator's size and this rank (ncclCommCount / ncclCommUserRank, rccl.h:378,400): what RCCL
+ * itself saw, so a harness can prove its world size (bench.py's rccl_world). */
+QGEMM_API int qgemm_comm_count(void *comm, int *count);
+QGEMM_API int qgemm_comm_user_rank(void *comm, int *rank);
 
 /* In-place all-gather of C's row shards over RCCL: on entry rank r holds rows
  * qgemm_shard_rows(m, world, r) of C (m x n row-major fp32, leading dimension n); on completion every
@@ -59,6 +63,27 @@ QGEMM_API int qgemm_allgather_rows(float *C, int m, int n, int world, int rank, 
  * C + first[i] + r*count[i], everyone receives C + first[i] .. + world*count[i]); root[i] >= 0 is an
  * in-place broadcast of [first[i], first[i] + count[i]) from rank root[i]. */
 QGEMM_API int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count, int *root, int max_ops);
+
+/* Pipelined whole-node step ("optionally pipeline the gather per row-chunk").  Rank r's rows
+ * qgemm_shard_rows(m, world, r) are split into `chunks` balanced pieces (qgemm_shard_rows(rows, chunks, c));
+ * chunk c of every rank is gathered by one in-place ncclBroadcast per owner (inside one group per chunk)
+ * while chunk c + 1 computes.  The plan as data (no GPU, no RCCL), chunk-major, owners ascending, owners with
+ * no rows in a chunk skipped: op i broadcasts count[i] floats at element first[i] of C from rank root[i].
+ * Unlike qgemm_allgather_plan it also lists the broadcasts at world == 1 (each then an in-place no-op), so
+ * the RCCL calls run on a one-GPU box.  Returns the number of operations (max_ops == 0 / NULL arrays: size
+ * query) or -hipErrorInvalidValue. */
+QGEMM_API int qgemm_allgather_chunk_plan(int m, int n, int world, int chunks, int64_t *first, int64_t *count,
+                                         int *root, int max_ops);
+/* Bytes of device workspace op_mm_quantize_shard_pipelined needs (B packed once + one chunk's A pack). */
+QGEMM_API size_t op_mm_quantize_shard_pipelined_workspace_size(int m, int n, int k, int world, int chunks);
+/* This rank's shard of op_mm_quantize(A, B, C, m, n, k) with the all-gather of C pipelined under it: B is
+ * packed once (qgemm_pack_b), chunk c's rows run op_mm_quantize_prepacked_ws on `stream` (bit-identical to
+ * op_mm_quantize_shard), then an event hands chunk c to `gather_stream`, where the chunk's broadcasts
+ * (qgemm_allgather_chunk_plan) run under chunk c + 1's compute.  On return `stream` waits for the last
+ * broadcast, so work enqueued after it sees the whole C.  comm may be NULL only when world == 1 (no gather). */
+QGEMM_API int op_mm_quantize_shard_pipelined(const float *A, const float *B, float *C, int m, int n, int k, int world,
+                                             int rank, int chunks, void *comm, void *workspace, size_t ws_bytes,
+                                             void *stream, void *gather_stream);
 
 /* One planned collective of the one-process node path: on device index `rank`, root < 0 is an in-place
  * ncclAllGather (send C + send_off, receive C + recv_off .. + ndev * count), root >= 0 an in-place

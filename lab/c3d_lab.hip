@@ -6,7 +6,7 @@
 //      non-temporal loads of W and X in pass 2; 4: order 2 with non-temporal loads of X only
 //   G  gemm_i8_fm split-K 2 with both slabs (rounds 2-3) | ticket-first (one slab, uneven K split: round 4) |
 //      fk (gemm_i8_fk: split-K inside the CU)
-//   build/c3d_lab m n k rounds
+//   build/c3d_lab m n k rounds [sync|orders]   (sync: the product vs kSync, twice the product as a noise floor)
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -75,8 +75,9 @@ int main(int argc, char **argv) {
             pack_cols_kernel<true, kTilesPerBlock, false><<<g2, 256, 0, s0>>>(W, n, k, n, range, vw.scratch, vw.parts,
                                                                               vw.rows_pad, vw.scale, vw.q, vw.k_pad);
     };
-    // g: 0 = fm split-K both slabs (rounds 2-3), 1 / 2 = ticket-first split-K with slice 0 = 30 / 31 of 64 k-steps,
-    // 3 = fk (split-K inside the CU), 4 = ticket-first 31 with the XCD-pair map
+    // g: 0 / 2 = ticket-first split-K with slice 0 = 31 of 64 k-steps (the product; the rounds 2-3 both-slabs form and the
+    // XCD-pair map are lab/splitk_both_pairxcd_experiment.patch), 1 = slice 0 = 30, 3 = fk (split-K inside the CU),
+    // 4 = ticket-first 31 with an s_barrier every 3 sub-steps (kSync, round 5)
     auto gemm = [&](int g, float *out) {
         GemmArgs p{};
         p.A = vx.q; p.B = vw.q; p.Cx = vx.scale; p.Cw = vw.scale; p.C = out; p.csh = n; p.csw = 1; p.m = m; p.n = n;
@@ -87,13 +88,16 @@ int main(int argc, char **argv) {
             return;
         }
         p.tiles_n = tiles_n; p.splits = 2; p.slabs = slabs; p.tickets = tickets; p.reset_tickets = 1;
-        if (g == 0) gemm_i8_fm<kEpiNone, false, kSplitBoth><<<tiles * 2, 256, 0, s0>>>(p);
+        if (g == 0) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31><<<tiles * 2, 256, 0, s0>>>(p);
         if (g == 1) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 30><<<tiles * 2, 256, 0, s0>>>(p);
         if (g == 2) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31><<<tiles * 2, 256, 0, s0>>>(p);
-        if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);
+        if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);  // kSync
     };
     struct V { std::string name; int order; int g; };
-    std::vector<V> vs = {{"wonly_default", 2, 2}, {"product_nt", 3, 2}, {"nt_fk", 3, 3}, {"nt_both_slabs", 3, 0}};
+    std::vector<V> vs;
+    const std::string set = argc > 5 ? argv[5] : "sync";
+    if (set == "sync") vs = {{"product_nt", 3, 2}, {"nt_sync", 3, 4}, {"product_nt_b", 3, 0}};
+    else vs = {{"wonly_default", 2, 2}, {"product_nt", 3, 2}, {"nt_fk", 3, 3}};
     // reference: the library's order
     pass1(0); pass2(0); gemm(0, Cref);
     CK(hipStreamSynchronize(s0));

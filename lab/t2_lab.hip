@@ -45,7 +45,6 @@ static Variant make(const std::string &spec) {
     int a = 0, b = 0;
     if (spec == "fm") { v.fn = gemm_i8_fm<>; v.threads = 256; v.stamped = false; }
     else if (spec == "fmrot") { v.fn = gemm_i8_fm<>; v.threads = 256; v.stamped = false; v.kind = 3; }
-    else if (spec == "fms") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitBoth>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fk") { v.fn = gemm_i8_fk<>; v.threads = 256; v.stamped = false; v.kind = 2; }
     else if (spec == "fmf28") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 28>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fmf30") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 30>; v.threads = 256; v.stamped = false; v.kind = 1; }

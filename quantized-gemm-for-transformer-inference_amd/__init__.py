@@ -77,8 +77,13 @@ DIST_EXPORTED_SYMBOLS = (
     "qgemm_comm_init_rank",
     "qgemm_comm_init_all",
     "qgemm_comm_destroy",
+    "qgemm_comm_count",
+    "qgemm_comm_user_rank",
     "qgemm_allgather_rows",
     "qgemm_allgather_plan",
+    "qgemm_allgather_chunk_plan",
+    "op_mm_quantize_shard_pipelined_workspace_size",
+    "op_mm_quantize_shard_pipelined",
     "qgemm_node_allgather_plan",
     "qgemm_node_mm_quantize",
 )
@@ -202,11 +207,22 @@ def load_dist() -> ctypes.CDLL:
         D.qgemm_comm_init_all.restype = i32
         D.qgemm_comm_destroy.argtypes = [vp]
         D.qgemm_comm_destroy.restype = i32
+        D.qgemm_comm_count.argtypes = [vp, ctypes.POINTER(i32)]
+        D.qgemm_comm_count.restype = i32
+        D.qgemm_comm_user_rank.argtypes = [vp, ctypes.POINTER(i32)]
+        D.qgemm_comm_user_rank.restype = i32
         D.qgemm_allgather_rows.argtypes = [vp, i32, i32, i32, i32, vp, vp]
         D.qgemm_allgather_rows.restype = i32
         i64p = ctypes.POINTER(ctypes.c_int64)
         D.qgemm_allgather_plan.argtypes = [i32, i32, i32, i64p, i64p, ctypes.POINTER(i32), i32]
         D.qgemm_allgather_plan.restype = i32
+        D.qgemm_allgather_chunk_plan.argtypes = [i32, i32, i32, i32, i64p, i64p, ctypes.POINTER(i32), i32]
+        D.qgemm_allgather_chunk_plan.restype = i32
+        D.op_mm_quantize_shard_pipelined_workspace_size.argtypes = [i32, i32, i32, i32, i32]
+        D.op_mm_quantize_shard_pipelined_workspace_size.restype = ctypes.c_size_t
+        D.op_mm_quantize_shard_pipelined.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, ctypes.c_size_t,
+                                                     vp, vp]
+        D.op_mm_quantize_shard_pipelined.restype = i32
         D.qgemm_node_allgather_plan.argtypes = [i32, i32, i32, ctypes.POINTER(CollOp), i32]
         D.qgemm_node_allgather_plan.restype = i32
         D.qgemm_node_mm_quantize.argtypes = [vp, vp, vp, i32, i32, i32, i32, ctypes.POINTER(i32), vp, vp, i32]
@@ -254,6 +270,45 @@ def allgather_plan(m: int, n: int, world: int) -> list:
     return [(first[i], count[i], root[i]) for i in range(ops)]
 
 
+def allgather_chunk_plan(m: int, n: int, world: int, chunks: int) -> list:
+    """The broadcasts op_mm_quantize_shard_pipelined issues, chunk-major, as [(first, count, root)]
+    (qgemm_allgather_chunk_plan): each moves `count` floats at element `first` of C from rank `root`."""
+    D = load_dist()
+    cnt = D.qgemm_allgather_chunk_plan(m, n, world, chunks, None, None, None, 0)
+    if cnt < 0:
+        raise QGemmError("qgemm_allgather_chunk_plan", -cnt)
+    cap = max(1, cnt)
+    first, count, root = (ctypes.c_int64 * cap)(), (ctypes.c_int64 * cap)(), (ctypes.c_int * cap)()
+    got = D.qgemm_allgather_chunk_plan(m, n, world, chunks, first, count, root, cap)
+    if got != cnt:
+        raise QGemmError("qgemm_allgather_chunk_plan", -got if got < 0 else 1)
+    return [(first[i], count[i], root[i]) for i in range(cnt)]
+
+
+def op_mm_quantize_shard_pipelined(A, B, C, world: int, rank: int, chunks: int, comm=None, gather_stream=None,
+                                   workspace=None) -> None:
+    """op_mm_quantize_shard with the all-gather of C pipelined under the chunks' compute
+    (op_mm_quantize_shard_pipelined): on return (stream order) every rank's C holds all rows."""
+    import torch
+    for t, nm in ((A, "A"), (B, "B"), (C, "C")):
+        _require_device_f32(t, nm)
+        assert t.is_contiguous(), f"{nm} must be contiguous row-major"
+    M, K = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == K and C.shape == (M, N), "A m x k, B k x n, C m x n"
+    D = load_dist()
+    need = D.op_mm_quantize_shard_pipelined_workspace_size(M, N, K, world, chunks)
+    if workspace is None:
+        workspace = torch.empty(need, dtype=torch.uint8, device=A.device)
+    assert workspace.numel() >= need, "workspace too small"
+    s = _stream(A.device)
+    g = ctypes.c_void_p(gather_stream.cuda_stream) if gather_stream is not None else s  # a torch.cuda.Stream
+    _check("op_mm_quantize_shard_pipelined",
+           D.op_mm_quantize_shard_pipelined(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, world, rank, chunks,
+                                            comm.handle if comm is not None else None, workspace.data_ptr(),
+                                            workspace.numel(), s, g))
+
+
 def op_mm_quantize_shard(A, B, C, world: int, rank: int) -> None:
     """Rows [m0, m0 + rows) of C = op_mm_quantize(A, B) on this rank (per-rank pointer offsets into the
     full row-major A and C; bit-identical to those rows of the one-GPU call)."""
@@ -291,6 +346,17 @@ class Comm:
         _check("qgemm_allgather_rows", load_dist().qgemm_allgather_rows(C.data_ptr(), C.shape[0], C.shape[1], self.world,
                                                                         self.rank, self.handle, _stream(C.device)))
 
+    def count(self) -> int:
+        """The communicator's size as RCCL reports it (ncclCommCount)."""
+        c = ctypes.c_int(-1)
+        _check("qgemm_comm_count", load_dist().qgemm_comm_count(self.handle, ctypes.byref(c)))
+        return c.value
+
+    def user_rank(self) -> int:
+        r = ctypes.c_int(-1)
+        _check("qgemm_comm_user_rank", load_dist().qgemm_comm_user_rank(self.handle, ctypes.byref(r)))
+        return r.value
+
     def close(self) -> None:
         if self.handle:
             _check("qgemm_comm_destroy", load_dist().qgemm_comm_destroy(self.handle))
@@ -299,6 +365,39 @@ class Comm:
 
 def version() -> str:
     return load().qgemm_version().decode()
+
+
+def source_hash() -> str:
+    """The Makefile's SRC_HASH recomputed from this tree: sha256 of the Makefile, csrc/*.{hip,h,cpp} and include/*.h
+    concatenated in sorted path order (make's $(sort) of the same relative paths), first 16 hex digits."""
+    import glob
+    import hashlib
+    rel = ["Makefile"]
+    for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.cpp", "../include/*.h"):
+        rel += [os.path.relpath(p, PKG_DIR) for p in glob.glob(os.path.join(PKG_DIR, pat))]
+    h = hashlib.sha256()
+    for r in sorted(rel):
+        with open(os.path.join(PKG_DIR, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def binary_hash() -> str:
+    """The source hash compiled into the loaded libqgemm.so (the `src=` field of qgemm_version())."""
+    for field in version().split():
+        if field.startswith("src="):
+            return field[4:]
+    return "none"
+
+
+def check_binary() -> str:
+    """Refuse a libqgemm.so built from other sources than this tree's (a stale build/ shipped with the
+    snapshot): returns the hash, raises RuntimeError on a mismatch."""
+    want, got = source_hash(), binary_hash()
+    if got != want:
+        raise RuntimeError(f"{LIB_PATH} was built from sources src={got}, this tree is src={want}: rebuild "
+                           "(make -C quantized-gemm-for-transformer-inference_amd all)")
+    return got
 
 
 def _check(fn: str, rc: int) -> None:

@@ -369,9 +369,13 @@ int qgemm_gemm_plan(int m, int n, int k, int *tile, const char **kernel) {
     return gemm_plan_info(m, n, round_up(k, kKPad), tile, kernel);
 }
 
+#ifndef QGEMM_SRC_HASH
+#define QGEMM_SRC_HASH "unknown"
+#endif
+
 const char *qgemm_version(void) {
-    static char buf[160];
-    snprintf(buf, sizeof buf, "qgemm 0.1.0 gfx950 %s", gemm_config_name());
+    static char buf[192];
+    snprintf(buf, sizeof buf, "qgemm 0.1.0 gfx950 %s src=%s", gemm_config_name(), QGEMM_SRC_HASH);
     return buf;
 }
 

@@ -64,6 +64,16 @@ int qgemm_comm_destroy(void *comm) {
     return nccl_rc(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
 }
 
+int qgemm_comm_count(void *comm, int *count) {
+    if (!comm || !count) return (int)hipErrorInvalidValue;
+    return nccl_rc(ncclCommCount(static_cast<ncclComm_t>(comm), count));
+}
+
+int qgemm_comm_user_rank(void *comm, int *rank) {
+    if (!comm || !rank) return (int)hipErrorInvalidValue;
+    return nccl_rc(ncclCommUserRank(static_cast<ncclComm_t>(comm), rank));
+}
+
 int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count, int *root, int max_ops) {
     if (m < 0 || n < 0 || world < 1 || max_ops < 0 || (max_ops > 0 && (!first || !count || !root)))
         return -(int)hipErrorInvalidValue;
@@ -90,6 +100,107 @@ int qgemm_allgather_plan(int m, int n, int world, int64_t *first, int64_t *count
         ++ops;
     }
     return ops;
+}
+
+namespace {
+
+// the chunked plan, chunk-major, owners ascending; chunk_of (optional) records each op's chunk
+int chunk_plan(int m, int n, int world, int chunks, int64_t *first, int64_t *count, int *root, int *chunk_of,
+               int max_ops) {
+    const bool query = first == nullptr;
+    int ops = 0;
+    for (int c = 0; c < chunks; ++c)
+        for (int r = 0; r < world; ++r) {
+            int m0 = 0, rows = 0, c0 = 0, crows = 0;
+            qgemm_shard_rows(m, world, r, &m0, &rows);
+            qgemm_shard_rows(rows, chunks, c, &c0, &crows);
+            if (crows == 0 || n == 0) continue;
+            if (!query) {
+                if (ops >= max_ops) return -(int)hipErrorInvalidValue;
+                first[ops] = (int64_t)(m0 + c0) * n;
+                count[ops] = (int64_t)crows * n;
+                root[ops] = r;
+                if (chunk_of) chunk_of[ops] = c;
+            }
+            ++ops;
+        }
+    return ops;
+}
+
+}  // namespace
+
+int qgemm_allgather_chunk_plan(int m, int n, int world, int chunks, int64_t *first, int64_t *count, int *root,
+                               int max_ops) {
+    if (m < 0 || n < 0 || world < 1 || chunks < 1 || max_ops < 0) return -(int)hipErrorInvalidValue;
+    if (max_ops == 0 || !first || !count || !root) return chunk_plan(m, n, world, chunks, nullptr, nullptr, nullptr,
+                                                                     nullptr, 0);
+    return chunk_plan(m, n, world, chunks, first, count, root, nullptr, max_ops);
+}
+
+size_t op_mm_quantize_shard_pipelined_workspace_size(int m, int n, int k, int world, int chunks) {
+    if (m < 0 || n < 1 || k < 1 || world < 1 || chunks < 1) return 0;
+    // the largest chunk any rank computes: ceil(ceil(m / world) / chunks) rows
+    const int rows = (m + world - 1) / world, crows = (rows + chunks - 1) / chunks;
+    const size_t pb = (qgemm_packed_size(n, k) + 255) / 256 * 256;
+    return pb + op_mm_quantize_prepacked_workspace_size(crows > 0 ? crows : 1, n, k);
+}
+
+int op_mm_quantize_shard_pipelined(const float *A, const float *B, float *C, int m, int n, int k, int world, int rank,
+                                   int chunks, void *comm, void *workspace, size_t ws_bytes, void *stream,
+                                   void *gather_stream) {
+    int m0 = 0, rows = 0;
+    const int e = qgemm_shard_rows(m, world, rank, &m0, &rows);
+    if (e) return e;
+    if (!A || !B || !C || n < 1 || k < 1 || chunks < 1 || !workspace || (world > 1 && !comm))
+        return (int)hipErrorInvalidValue;
+    if (ws_bytes < op_mm_quantize_shard_pipelined_workspace_size(m, n, k, world, chunks))
+        return (int)hipErrorInvalidValue;
+    const int nops = chunk_plan(m, n, world, chunks, nullptr, nullptr, nullptr, nullptr, 0);
+    std::vector<int64_t> first((size_t)nops + 1), count((size_t)nops + 1);
+    std::vector<int> root((size_t)nops + 1), chunk_of((size_t)nops + 1);
+    if (nops > 0 &&
+        chunk_plan(m, n, world, chunks, first.data(), count.data(), root.data(), chunk_of.data(), nops) != nops)
+        return (int)hipErrorInvalidValue;
+    hipStream_t s = static_cast<hipStream_t>(stream), g = static_cast<hipStream_t>(gather_stream);
+    ncclComm_t cm = static_cast<ncclComm_t>(comm);
+    const size_t pb_bytes = (qgemm_packed_size(n, k) + 255) / 256 * 256;
+    char *ws = static_cast<char *>(workspace);
+    // W packed ONCE for every chunk (the prepacked drop-in is bit-identical to op_mm_quantize)
+    int rc = qgemm_pack_b(B, n, 1, k, n, 127.0f, ws, s);
+    if (rc) return rc;
+    hipEvent_t ev = nullptr;
+    hipError_t he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (he != hipSuccess) return (int)he;
+    int op = 0;
+    for (int c = 0; c < chunks && rc == 0; ++c) {
+        int c0 = 0, crows = 0;
+        qgemm_shard_rows(rows, chunks, c, &c0, &crows);
+        if (crows > 0)
+            rc = op_mm_quantize_prepacked_ws(A + (int64_t)(m0 + c0) * k, k, ws, C + (int64_t)(m0 + c0) * n, n, crows,
+                                             n, k, ws + pb_bytes, ws_bytes - pb_bytes, s);
+        // this chunk's broadcasts (every owner's chunk c) on the gather stream, behind this rank's compute of it;
+        // the event is re-recorded per chunk: hipStreamWaitEvent captures the record it follows
+        const int o0 = op;
+        while (op < nops && chunk_of[(size_t)op] == c) ++op;
+        if (rc || !cm || op == o0) continue;
+        if ((he = hipEventRecord(ev, s)) != hipSuccess || (he = hipStreamWaitEvent(g, ev, 0)) != hipSuccess) {
+            rc = (int)he;
+            break;
+        }
+        ncclResult_t r = ncclGroupStart();
+        for (int i = o0; i < op && r == ncclSuccess; ++i)
+            r = ncclBroadcast(C + first[(size_t)i], C + first[(size_t)i], (size_t)count[(size_t)i], ncclFloat32,
+                              root[(size_t)i], cm, g);
+        const ncclResult_t r2 = ncclGroupEnd();
+        rc = nccl_rc(r != ncclSuccess ? r : r2);
+    }
+    // the caller's stream sees the whole C: it waits for the last broadcast
+    if (rc == 0 && cm && op > 0) {
+        if ((he = hipEventRecord(ev, g)) != hipSuccess || (he = hipStreamWaitEvent(s, ev, 0)) != hipSuccess)
+            rc = (int)he;
+    }
+    (void)hipEventDestroy(ev);  // released once its last record completes
+    return rc;
 }
 
 int qgemm_node_allgather_plan(int m, int n, int ndev, qgemm_coll_op *ops, int max_ops) {
@@ -176,6 +287,10 @@ int qgemm_node_mm_quantize(const float *const *A, const float *const *B, float *
             const int got = qgemm_node_allgather_plan(m, n, ndev, ops.data(), nops);
             if (got < 0) rc = -got;
         }
+        // every device is selected once BEFORE the group opens, so the only fallible steps inside it are the
+        // enqueues themselves (a failure there leaves the communicators unusable, as any RCCL group error does)
+        for (int r = 0; r < ndev && rc == 0 && nops > 0; ++r)
+            if ((he = hipSetDevice(devices[r])) != hipSuccess) rc = (int)he;
         if (rc == 0 && nops > 0) {
             ncclResult_t g = ncclGroupStart();
             for (int i = 0; i < nops && rc == 0 && g == ncclSuccess; ++i) {

@@ -167,39 +167,8 @@ __device__ __forceinline__ const int8_t *uniform_ptr(const int8_t *q) {
 
 constexpr int kFmThreads = 256;
 
-// Split-K arrival for gemm_i8_fm (two K slices per tile, the only split the 256-tile plan makes): the same
-// write-through protocol as splitk_combine -- this slice's AGPR accumulators stored to its slab with sc1
-// stores, drained, then a relaxed agent-scope ticket.  Returns true in the slice that arrives last; its
-// epilogue adds the other slab's partial sums (sc1 loads, after the ticket) as it reads the accumulators, so
-// no accumulator is copied out of the AGPRs.
-__device__ __forceinline__ bool splitk_arrive_fm(const GemmArgs &p, unsigned *last, v4i (&acc)[8][8], int tile,
-                                                 int slice, int wave, int lane, int tid) {
-    constexpr int S = 2;
-    constexpr int kSlabBytes = 4 * 8 * 8 * 64 * 16;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<char *>(p.slabs) + (int64_t)tile * S * kSlabBytes, 0, S * kSlabBytes, 0x00020000);
-    const int lane_off = (wave * 64 * 64 + lane) * 16;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni)
-            __builtin_amdgcn_raw_buffer_store_b128(acc[mi][ni], rsrc, slice * kSlabBytes + lane_off + (mi * 8 + ni) * 1024,
-                                                   0, 16 /* sc1 */);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned t = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *last = t;
-        if (t == (unsigned)(S - 1) && p.reset_tickets)
-            __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    return *last == (unsigned)(S - 1);
-}
-
-// Split-K modes of gemm_i8_fm (two K slices per tile, the only split the 256-tile plan makes):
-//   kSplitBoth  : equal slices; each stores its slab and draws a ticket, the last arriver reads the other slab
-//                 (splitk_arrive_fm; rounds 2-3)
+// Split-K modes of gemm_i8_fm (two K slices per tile, the only split the 256-tile plan makes; the rounds 2-3
+// form where both slices stored a slab, and the XCD-pair map, are lab/splitk_both_pairxcd_experiment.patch):
 //   kSplitFirst : (round 4) the ticket FIRST: only the slice that arrives first stores its slab (sc1 stores,
 //                 drained, block barrier) and publishes it by adding 2 to the ticket; the second arriver stores
 //                 nothing, waits for the published value (ticket == 4 in either arrival order: 0 -> 1 -> 3 -> 4 or
@@ -209,14 +178,14 @@ __device__ __forceinline__ bool splitk_arrive_fm(const GemmArgs &p, unsigned *la
 //                 of the k-steps, so it normally arrives first and its slab has landed before slice 1's loop ends:
 //                 one slab per tile instead of two, off the critical path.  The waiting slice never waits on a
 //                 block that is not running: the first arriver has already drawn its ticket.
-enum SplitMode { kSplitNone = 0, kSplitBoth = 1, kSplitFirst = 2 };
+enum SplitMode { kSplitNone = 0, kSplitFirst = 2 };
 
 // kNtC: the full-tile output stores are nontemporal (C2 bench, one box, interleaved: 11 598 vs 11 431 GEMMs/s, GEMM
 // 58.2 vs 59.5 us by events; profiles/r03_ab_nt_c.log) -- the 64-MiB tail streams past the caches
-// kPairXcd (kSplitFirst only): blocks b and b + 8 share an XCD; XCD 2j takes K slice 0 and XCD 2j + 1 slice 1 of the
-// same 32 tiles (a 4 x 8 patch), so each XCD fetches 4 A + 8 B half-panels instead of 4 + 4 whole panels
+// kSync: an s_barrier at the top of every 3-sub-step trip keeps the CU's 4 waves within one trip of each other
+// (lab/w4_lab.hip `f4sync`: +0.9 us at K 4096, -3.4 at 8192, -5.3 at 16384, profiles/r03_f4_sync_longk.log)
 template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30,
-          bool kPairXcd = false>
+          bool kSync = false>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
@@ -232,14 +201,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     // operand fetch 404.7 -> 337.6 MB but ran 127.3 us vs 122-126 (the slab then crosses XCDs)
     const int S = kSplit ? 2 : 1;  // the 256-tile plan splits in two or not at all (host checks)
     const int wid = xcd_remap(blockIdx.x, gridDim.x);
-    int tile = wid / S, slice = wid - tile * S;
-    if constexpr (kPairXcd) {
-        static_assert(kSplit == kSplitFirst, "the XCD-pair map needs the write-through ticket-first hand-off");
-        // gridDim.x = 256 (the split plan runs at exactly 128 tiles): 32 blocks per XCD
-        const int xcd = blockIdx.x & 7;
-        tile = (xcd >> 1) * 32 + (blockIdx.x >> 3);
-        slice = xcd & 1;
-    }
+    const int tile = wid / S, slice = wid - tile * S;
     int tm, tn;
     group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
     const int nsub = (int)(p.k_pad / 64);
@@ -302,6 +264,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     for (int j = 0; j < 16; ++j) ld(a1, b1, j, nloc > 1 ? 1 : 0);
     int u = 0;
     for (; u + 3 <= nloc; u += 3) {
+        if constexpr (kSync) __builtin_amdgcn_s_barrier();
         substep(a0, b0, a2, b2, u + 2, true);
         substep(a1, b1, a0, b0, u + 3, true);
         substep(a2, b2, a1, b1, u + 4, true);
@@ -313,15 +276,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     }
     // the last MFMAs' results are read by VALU below; the asm statements hide them from hipcc's padding
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-    if constexpr (kSplit == kSplitBoth) {
-        {
-            // split-K: slabs + arrival ticket (write-through form, see splitk_combine); the last slice of
-            // the tile holds the complete sums and runs the epilogue
-            unsigned *last = reinterpret_cast<unsigned *>(lds + 4 * kBlockBytes + 2048);
-            if (!splitk_arrive_fm(p, last, acc, tile, slice, wave, lane, tid)) return;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: slab loads stay below
-        }
-    } else if constexpr (kSplit == kSplitFirst) {
+    if constexpr (kSplit == kSplitFirst) {
         unsigned *last = reinterpret_cast<unsigned *>(lds + 4 * kBlockBytes + 2048);
         if (tid == 0) *last = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -403,9 +358,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         if constexpr (kSplit) {
             constexpr int kSlabBytes = 4 * 8 * 8 * 64 * 16;
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<char *>(p.slabs) +
-                    (kSplit == kSplitFirst ? (int64_t)tile : (int64_t)tile * 2 + (1 - slice)) * kSlabBytes,
-                0, kSlabBytes, 0x00020000);
+                reinterpret_cast<char *>(p.slabs) + (int64_t)tile * kSlabBytes, 0, kSlabBytes, 0x00020000);
             const int lane_off = (wave * 64 * 64 + lane) * 16;
 #pragma unroll
             for (int mq = 0; mq < 4; ++mq)

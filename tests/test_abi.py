@@ -258,3 +258,82 @@ def test_allgather_plan_has_no_world_cap(qg):
     assert len(qg.allgather_plan(129, 2, 128)) == 128
     D = qg.load_dist()
     assert D.qgemm_allgather_rows(None, 512, 2, 128, 0, None, None) == 1  # still the argument check, not a cap
+
+
+def _copy_tree(qg, dst):
+    """The package's hashed sources + its built library, laid out as in the repo (pkg/ beside include/)."""
+    import shutil
+    pkg = dst / "pkg"
+    shutil.copytree(os.path.join(qg.PKG_DIR, "csrc"), pkg / "csrc")
+    shutil.copy(os.path.join(qg.PKG_DIR, "Makefile"), pkg / "Makefile")
+    shutil.copy(os.path.join(qg.PKG_DIR, "__init__.py"), pkg / "__init__.py")
+    shutil.copytree(os.path.join(REPO, "include"), dst / "include")
+    (pkg / "build").mkdir()
+    shutil.copy(qg.LIB_PATH, pkg / "build" / "libqgemm.so")
+    return pkg
+
+
+def _load_copy(pkg, name):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(name, str(pkg / "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_binary_carries_this_trees_source_hash(qg):
+    """qgemm_version() names the sources it was built from (Makefile SRC_HASH) and they are this tree's."""
+    h = qg.source_hash()
+    assert len(h) == 16 and f"src={h}" in qg.version()
+    assert qg.check_binary() == h
+
+
+def test_stale_binary_is_rejected(qg, tmp_path):
+    """A build/ compiled from other sources (here: one source edited after the build) is refused by
+    check_binary(), which smoke() and bench.py call before any timing."""
+    pkg = _copy_tree(qg, tmp_path)
+    fresh = _load_copy(pkg, "qgemm_copy_fresh")
+    assert fresh.source_hash() == qg.source_hash() and fresh.check_binary() == qg.source_hash()
+    with open(pkg / "csrc" / "api.hip", "a") as f:
+        f.write("\n// edited after the build\n")
+    stale = _load_copy(pkg, "qgemm_copy_stale")
+    assert stale.source_hash() != qg.source_hash()
+    with pytest.raises(RuntimeError, match="built from sources"):
+        stale.check_binary()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("chunks", [1, 2, 3, 4])
+def test_chunked_allgather_plan_assembles_every_rank(qg, world, chunks):
+    """op_mm_quantize_shard_pipelined's broadcasts (qgemm_allgather_chunk_plan), executed on per-rank
+    buffers: chunk-major, each op is its root's own rows of that chunk, every row is moved exactly once,
+    and every rank ends with the whole C -- for m % world != 0, m < world, m % chunks != 0."""
+    import numpy as np
+    n = 3
+    for m in (0, 1, world - 1, 7, 65, 1001, 65536 + 3):
+        plan = qg.allgather_chunk_plan(m, n, world, chunks)
+        owner = np.full(m, -1)
+        for r in range(world):
+            m0, rows = qg.shard_rows(m, world, r)
+            owner[m0:m0 + rows] = r
+        seen = np.zeros(m, dtype=int)
+        last_chunk = -1
+        bufs = [np.full(m * n, np.nan) for _ in range(world)]
+        for r in range(world):  # each rank holds only its own rows before the gather
+            m0, rows = qg.shard_rows(m, world, r)
+            bufs[r][m0 * n:(m0 + rows) * n] = np.arange(m0 * n, (m0 + rows) * n)
+        for first, count, root in plan:
+            assert first % n == 0 and count % n == 0 and count > 0
+            r0, rr = first // n, count // n
+            assert (owner[r0:r0 + rr] == root).all(), "a broadcast moves its root's own rows"
+            m0, rows = qg.shard_rows(m, world, root)
+            c = [ci for ci in range(chunks) if qg.shard_rows(rows, chunks, ci)[0] + m0 == r0][0]
+            assert c >= last_chunk, "chunk-major order"
+            last_chunk = c
+            seen[r0:r0 + rr] += 1
+            for b in bufs:  # in place: receive = send region on every rank
+                b[first:first + count] = bufs[root][first:first + count]
+        assert (seen == 1).all(), (m, world, chunks)
+        for b in bufs:
+            assert np.array_equal(b, np.arange(m * n, dtype=float))
+        assert len(plan) <= world * chunks

@@ -41,6 +41,41 @@ def test_rccl_comm_and_allgather_one_rank(qg, device):
         comm.close()
 
 
+@pytest.mark.parametrize("M,chunks", [(1000, 3), (4096, 2), (96, 5)])
+def test_pipelined_shard_gather_one_rank_bit_identical(qg, oracle, device, M, chunks):
+    """op_mm_quantize_shard_pipelined at world 1: W packed once, the rows in chunks on the compute stream,
+    each chunk's (in-place, one-rank) ncclBroadcast on a second stream behind an event; the caller's stream
+    waits for the last one.  C must equal the one-GPU call bit for bit (optional pipelining)."""
+    N, K = 300, 520
+    X, W = oracle.inputs(M, N, K, 78)
+    Xd, Wd = torch.from_numpy(X).to(device), torch.from_numpy(W).to(device)
+    C = torch.full((M, N), float("nan"), device=device)
+    comm = qg.Comm(1, 0, qg.Comm.unique_id())
+    try:
+        assert comm.count() == 1 and comm.user_rank() == 0
+        g = torch.cuda.Stream(device)
+        qg.op_mm_quantize_shard_pipelined(Xd, Wd, C, 1, 0, chunks, comm=comm, gather_stream=g)
+        got = C.cpu().numpy()  # on torch's stream, which waits for the gather stream
+    finally:
+        comm.close()
+    assert_bits_equal(got, oracle.quantized_mm(X, W), f"pipelined, {chunks} chunks")
+
+
+def test_pipelined_shard_rejects_small_workspace_and_missing_comm(qg, device):
+    D = qg.load_dist()
+    A = torch.zeros((64, 32), device=device)
+    B = torch.zeros((32, 16), device=device)
+    C = torch.zeros((64, 16), device=device)
+    need = D.op_mm_quantize_shard_pipelined_workspace_size(64, 16, 32, 2, 2)
+    ws = torch.empty(need, dtype=torch.uint8, device=device)
+    s = qg._stream(device)
+    assert D.op_mm_quantize_shard_pipelined(A.data_ptr(), B.data_ptr(), C.data_ptr(), 64, 16, 32, 1, 0, 2, None,
+                                            ws.data_ptr(), need - 1, s, s) == qg.HIP_ERROR_INVALID_VALUE
+    # world 2 without a communicator: nothing to gather with
+    assert D.op_mm_quantize_shard_pipelined(A.data_ptr(), B.data_ptr(), C.data_ptr(), 64, 16, 32, 2, 0, 2, None,
+                                            ws.data_ptr(), need, s, s) == qg.HIP_ERROR_INVALID_VALUE
+
+
 def test_cpp_multi_gpu_driver_one_gpu():
     """timing_quantize -g: shard compute + RCCL all-gather timed, every C bit-equal to one-GPU."""
     out = subprocess.run([os.path.join(BUILD, "timing_quantize"), "-m", "1024", "-n", "768", "-k", "512", "-r", "3",
