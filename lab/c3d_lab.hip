@@ -91,12 +91,13 @@ int main(int argc, char **argv) {
         if (g == 0) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31><<<tiles * 2, 256, 0, s0>>>(p);
         if (g == 1) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 30><<<tiles * 2, 256, 0, s0>>>(p);
         if (g == 2) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31><<<tiles * 2, 256, 0, s0>>>(p);
-        if (g == 4) gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true><<<tiles * 2, 256, 0, s0>>>(p);  // kSync
+        // g == 4: the product header's kSync knob (an s_barrier every 3 sub-steps), measured neutral in round 5
+        // (profiles/r05_c3d_sync.log: GEMM 109.15 vs 108.93-108.95 us) and removed; lab/fm_sync_experiment.patch
     };
     struct V { std::string name; int order; int g; };
     std::vector<V> vs;
     const std::string set = argc > 5 ? argv[5] : "sync";
-    if (set == "sync") vs = {{"product_nt", 3, 2}, {"nt_sync", 3, 4}, {"product_nt_b", 3, 0}};
+    if (set == "sync") vs = {{"product_nt", 3, 2}, {"product_nt_b", 3, 0}};
     else vs = {{"wonly_default", 2, 2}, {"product_nt", 3, 2}, {"nt_fk", 3, 3}};
     // reference: the library's order
     pass1(0); pass2(0); gemm(0, Cref);

@@ -1,0 +1,104 @@
+// maskpack_lab.hip -- LAB: where the LLM.int8() masked single-pass pack (pack_single_pass8_kernel<4, true>) spends the
+// time it adds over the plain pass (<5, false>): 33.1 vs 28.3 us in the round-4 c2_outlier trace.  Every variant runs
+// right after the product's flags launch (outlier_flags_kernel with the fused index), so all see the same cache
+// state (flags just read X); `alone` variants run back to back without it.  Variants:
+//   plain    <5, false>                         (no mask at all)
+//   mask     <4, true>, 8 outlier columns       (the product)
+//   mask5    <5, true>, 8 outlier columns       (the round-2 register budget)
+//   mask0    <4, true>, no outlier column       (the mask machinery alone: count 0)
+// Interleaved rounds, events around each launch; the outputs of mask / mask5 compared bit for bit.
+//   build/maskpack_lab [m n k rounds]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/outlier.hip"
+#include "../quantized-gemm-for-transformer-inference_amd/csrc/gemm_i8.hip"
+
+using namespace qgemm;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+__global__ void put_outliers(float *X, int m, int k, int every, int ncols) {
+    // ncols columns spread over k (bench.py outlier_columns), every `every`-th row |x| = 30
+    const int c = blockIdx.x, i = threadIdx.x + blockIdx.y * 256;
+    if (c >= ncols || i * every >= m) return;
+    const int col = (k / ncols) * c + 7 * c + 3;
+    X[(int64_t)i * every * k + col] = (i & 1) ? 30.0f : -30.0f;
+}
+
+int main(int argc, char **argv) {
+    const int m = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 4096;
+    const int rounds = argc > 4 ? atoi(argv[4]) : 9, reps = 10;
+    float *X, *W; void *PX, *PW, *scr; unsigned *ticket;
+    CK(hipMalloc(&X, (size_t)m * k * 4)); CK(hipMalloc(&W, (size_t)k * n * 4));
+    CK(hipMalloc(&PX, packed_bytes(m, k))); CK(hipMalloc(&PW, packed_bytes(n, k)));
+    CK(hipMalloc(&scr, outlier_scratch_bytes(m, n, k))); CK(hipMalloc(&ticket, 256)); CK(hipMemset(ticket, 0, 256));
+    CK(launch_fill_uniform(X, (int64_t)m * k, 11, -1.f, 1.f, nullptr));
+    CK(launch_fill_uniform(W, (int64_t)k * n, 12, -1.f, 1.f, nullptr));
+    put_outliers<<<dim3(8, (m / 50 + 255) / 256 + 1), 256>>>(X, m, k, 50, 8);
+    CK(hipDeviceSynchronize());
+    const PackedView vx = packed_view(PX, m, k), vw = packed_view(PW, n, k);
+    const OutlierScratch v = scratch_view(scr, m, k);
+    hipStream_t s0; CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+    const int nstrips = n / kWs8Cols, npad = (int)((vw.rows_pad - n) / kWs8Cols), nx = (int)(vx.rows_pad / 8);
+    const int g = nstrips + npad + nx;
+    const int64_t wo_ld = round_up(n, 256);
+    const float range = 127.f;
+    auto flags = [&](float t) { CK(outlier_scan(X, k, m, k, t, v, ticket, s0)); };
+    const OutlierMask om{v.bits, v.rank, v.idx, v.xm, v.wm, wo_ld};
+    auto pack = [&](int var) {
+        if (var == 0)
+            pack_single_pass8_kernel<5><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n, n,
+                                                           vw.scale, vw.q, vw.rows_pad, nstrips, range, nullptr, 0);
+        else if (var == 2)
+            pack_single_pass8_kernel<5, true><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n,
+                                                                 n, vw.scale, vw.q, vw.rows_pad, nstrips, range, nullptr,
+                                                                 0, om);
+        else
+            pack_single_pass8_kernel<4, true><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n,
+                                                                 n, vw.scale, vw.q, vw.rows_pad, nstrips, range, nullptr,
+                                                                 0, om);
+    };
+    struct V { std::string name; int pack; float t; bool with_flags; };
+    std::vector<V> vs = {{"plain", 0, 6.f, true}, {"mask", 1, 6.f, true}, {"mask5", 2, 6.f, true},
+                         {"mask0", 1, 1e30f, true}, {"plain_alone", 0, 6.f, false}, {"mask_alone", 1, 6.f, false}};
+    // bit check: mask vs mask5
+    std::vector<int8_t> a(vx.rows_pad * vx.k_pad), b(a.size());
+    flags(6.f); pack(1); CK(hipStreamSynchronize(s0));
+    int cnt = 0; CK(hipMemcpy(&cnt, v.idx, 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(a.data(), vx.q, a.size(), hipMemcpyDeviceToHost));
+    CK(hipMemsetAsync(vx.q, 0x5a, a.size(), s0));
+    flags(6.f); pack(2); CK(hipStreamSynchronize(s0));
+    CK(hipMemcpy(b.data(), vx.q, b.size(), hipMemcpyDeviceToHost));
+    printf("outlier columns %d; mask5 vs mask X packed: %s\n", cnt, memcmp(a.data(), b.data(), a.size()) ? "DIFF" : "same");
+    hipEvent_t ev[3];
+    for (auto &e : ev) CK(hipEventCreate(&e));
+    for (int i = 0; i < 300; ++i) { flags(6.f); pack(1); }  // clocks up
+    std::vector<std::vector<float>> tf(vs.size()), tp(vs.size());
+    for (int r = 0; r < rounds; ++r)
+        for (size_t i = 0; i < vs.size(); ++i) {
+            const V &x = vs[i];
+            for (int w = 0; w < 3; ++w) { if (x.with_flags) flags(x.t); pack(x.pack); }
+            float af = 0, ap = 0;
+            for (int j = 0; j < reps; ++j) {
+                CK(hipEventRecord(ev[0], s0));
+                if (x.with_flags) flags(x.t);
+                CK(hipEventRecord(ev[1], s0));
+                pack(x.pack);
+                CK(hipEventRecord(ev[2], s0));
+                CK(hipEventSynchronize(ev[2]));
+                float y;
+                CK(hipEventElapsedTime(&y, ev[0], ev[1])); af += y;
+                CK(hipEventElapsedTime(&y, ev[1], ev[2])); ap += y;
+            }
+            tf[i].push_back(af * 1000 / reps); tp[i].push_back(ap * 1000 / reps);
+        }
+    auto med = [](std::vector<float> x) { std::sort(x.begin(), x.end()); return x[x.size() / 2]; };
+    for (size_t i = 0; i < vs.size(); ++i)
+        printf("%-12s flags %7.2f us  pack %7.2f us\n", vs[i].name.c_str(), med(tf[i]), med(tp[i]));
+    return 0;
+}

@@ -49,7 +49,6 @@ static Variant make(const std::string &spec) {
     else if (spec == "fmf28") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 28>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fmf30") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 30>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fmf31") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31>; v.threads = 256; v.stamped = false; v.kind = 1; }
-    else if (spec == "fmf31p") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 31, true>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "fmf32") { v.fn = gemm_i8_fm<kEpiNone, false, kSplitFirst, true, 32>; v.threads = 256; v.stamped = false; v.kind = 1; }
     else if (spec == "t2") { v.fn = gemm_i8_t2<kT2Nt>; v.sfn = gemm_i8_t2<kT2Nt | kT2Stamp>; }
     else if (spec == "t2plain") { v.fn = gemm_i8_t2<0>; v.sfn = gemm_i8_t2<kT2Stamp>; }

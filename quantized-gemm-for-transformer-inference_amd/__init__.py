@@ -368,12 +368,13 @@ def version() -> str:
 
 
 def source_hash() -> str:
-    """The Makefile's SRC_HASH recomputed from this tree: sha256 of the Makefile, csrc/*.{hip,h,cpp} and include/*.h
+    """The Makefile's SRC_HASH recomputed from this tree: sha256 of the Makefile, csrc/*.{hip,h,cpp}, include/*.h and
+    the harness sources src/*.cpp, src/*/*.{h,cuh}
     concatenated in sorted path order (make's $(sort) of the same relative paths), first 16 hex digits."""
     import glob
     import hashlib
     rel = ["Makefile"]
-    for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.cpp", "../include/*.h"):
+    for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.cpp", "../include/*.h", "src/*.cpp", "src/*/*.h", "src/*/*.cuh"):
         rel += [os.path.relpath(p, PKG_DIR) for p in glob.glob(os.path.join(PKG_DIR, pat))]
     h = hashlib.sha256()
     for r in sorted(rel):
@@ -388,6 +389,17 @@ def binary_hash() -> str:
         if field.startswith("src="):
             return field[4:]
     return "none"
+
+
+def file_hash(path: str = LIB_PATH) -> str:
+    """The source hash tagged inside a built libqgemm.so, read from the file (no dlopen): "" if absent."""
+    import re
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"QGEMM_SRC_HASH=([0-9a-f]{16})", f.read())
+    except OSError:
+        return ""
+    return m.group(1).decode() if m else ""
 
 
 def check_binary() -> str:

@@ -182,10 +182,7 @@ enum SplitMode { kSplitNone = 0, kSplitFirst = 2 };
 
 // kNtC: the full-tile output stores are nontemporal (C2 bench, one box, interleaved: 11 598 vs 11 431 GEMMs/s, GEMM
 // 58.2 vs 59.5 us by events; profiles/r03_ab_nt_c.log) -- the 64-MiB tail streams past the caches
-// kSync: an s_barrier at the top of every 3-sub-step trip keeps the CU's 4 waves within one trip of each other
-// (lab/w4_lab.hip `f4sync`: +0.9 us at K 4096, -3.4 at 8192, -5.3 at 16384, profiles/r03_f4_sync_longk.log)
-template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30,
-          bool kSync = false>
+template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
@@ -264,7 +261,6 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     for (int j = 0; j < 16; ++j) ld(a1, b1, j, nloc > 1 ? 1 : 0);
     int u = 0;
     for (; u + 3 <= nloc; u += 3) {
-        if constexpr (kSync) __builtin_amdgcn_s_barrier();
         substep(a0, b0, a2, b2, u + 2, true);
         substep(a1, b1, a0, b0, u + 3, true);
         substep(a2, b2, a1, b1, u + 4, true);

@@ -8,11 +8,11 @@
 //   Co  = fmaf chain from +0 over the outlier columns in ascending k: X[i,k] * W[k,j]
 //   O   = fl(O8 + Co)            (no outlier columns: O = O8, the plain path)
 //
-// One call, fast path (row-major operands on the single-pass pack + 256-tile GEMM): four launches --
+// One call, fast path (row-major operands on the single-pass pack + 256-tile GEMM): three launches --
 //   outlier_flags  : X read once in full-row float4 loads; per 64-row chunk a bitmask of its outlier
-//                    columns (every word written: nothing to clear per call)
-//   outlier_index  : one block ORs the chunk masks into the column mask, the per-word ranks, the
-//                    ascending list of outlier columns and their count (stays on the device)
+//                    columns (every word written: nothing to clear per call); the workgroup that arrives
+//                    last ORs the chunk masks into the column mask, the per-word ranks, the ascending list
+//                    of outlier columns and their count (stays on the device; round 5: no index launch)
 //   the pack       : the single pass with the mask (pack.hip): X'/W' quantized without materialising
 //                    them, the outlier columns' values written compactly (xo [m][cnt], wo [cnt][n_pad])
 //   the GEMM       : the int8 part with the fp32 chain added in its store epilogue (gemm_i8_kernels.h)
@@ -34,11 +34,76 @@ __device__ __forceinline__ bool is_outlier(float a, float b) {
     return !(((a >= 0) & (a <= b)) | ((a <= 0) & (-a <= b)));
 }
 
+// bits[w] = OR of the chunk masks, rank[w] = set bits below word w, idx[1 + ...] = the outlier columns in
+// ascending order, idx[0] = their count -- by the ONE workgroup of outlier_flags_kernel that arrives last.  P
+// adjacent threads share a word (each ORs every P-th chunk, 16 sc1 loads in flight, then a shuffle-OR),
+// kThreads / P words per pass; the ranks by a wave scan + a scan of the 4 wave sums.
+template <int P>
+__device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial, int nchunks, int nwords,
+                                            uint32_t *__restrict__ bits, int *__restrict__ rank, int *__restrict__ idx,
+                                            int *wsum, int *base) {
+    constexpr int kThreads = 256;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int s = tid % P;
+    int run = 0;  // count of outlier columns in the words already done (the same in every thread)
+    for (int w0 = 0; w0 < nwords; w0 += kThreads / P) {
+        const int w = w0 + tid / P;
+        uint32_t word = 0;
+        if (w < nwords) {
+            int ch = s;
+            // the partial words are the other workgroups' sc1 stores: every load of them is an sc1 load
+            for (; ch + 15 * P < nchunks; ch += 16 * P) {
+                uint32_t u[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    u[e] = __hip_atomic_load(partial + (int64_t)(ch + e * P) * nwords + w, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) word |= u[e];
+            }
+            for (; ch < nchunks; ch += P)
+                word |= __hip_atomic_load(partial + (int64_t)ch * nwords + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int off = 1; off < P; off <<= 1) word |= (uint32_t)__shfl_xor((int)word, off, 64);
+        const int pc = (s == 0 && w < nwords) ? __popc(word) : 0;
+        int x = pc;  // inclusive scan over the block in thread order (= word order)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(x, off, 64);
+            if (lane >= off) x += v;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        int before = run;
+        for (int j = 0; j < wave; ++j) before += wsum[j];
+        const int below = before + x - pc;
+        if (s == 0 && w < nwords) {
+            bits[w] = word;
+            rank[w] = below;
+            int j = 0;
+            for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
+        }
+        run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();  // wsum is rewritten by the next pass
+    }
+    if (tid == 0) *base = run;
+}
+
 // partial[chunk][word]: bit c of word w set when column 32w + c holds an outlier in rows
-// [64 chunk, 64 chunk + 64).  Thread t: columns 1024 bx + 4t .. +3.
-template <bool VEC>
+// [64 chunk, 64 chunk + 64).  Thread t: columns 1024 bx + 4t .. +3.  Then the workgroup that arrives last
+// (one agent-scope add per workgroup on *ticket, after every wave's sc1 partial stores have drained: the
+// write-through hand-off of MI355X_MICROARCH.md, row 1) builds the column mask, ranks, list and count
+// (build_index) and re-zeroes the ticket for the next call -- no separate index launch.  *ticket is
+// library-owned, zeroed once at allocation, one per (device, stream).
+template <bool VEC, int P>
 __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
-                                                            float t, uint32_t *__restrict__ partial, int nwords) {
+                                                            float t, uint32_t *__restrict__ partial, int nwords,
+                                                            unsigned *__restrict__ ticket, uint32_t *__restrict__ bits,
+                                                            int *__restrict__ rank, int *__restrict__ idx) {
+    __shared__ int wsum[4];
+    __shared__ unsigned last;
+    __shared__ int count;
     const int tid = threadIdx.x;
     const int c = blockIdx.x * kFlagCols + 4 * tid;
     const int r0 = blockIdx.y * kChunkRows, r1 = min(m, r0 + kChunkRows);
@@ -65,66 +130,23 @@ __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restr
     word |= __shfl_xor(word, 2, 64);
     word |= __shfl_xor(word, 4, 64);
     const int w = blockIdx.x * (kFlagCols / 32) + (tid >> 3);
-    if ((tid & 7) == 0 && w < nwords) partial[(int64_t)blockIdx.y * nwords + w] = word;
-}
-
-// bits[w] = OR of the chunk masks, rank[w] = set bits below word w, idx[1 + ...] = the outlier columns in
-// ascending order, idx[0] = their count.  One block; P adjacent threads share a word (each ORs every P-th
-// chunk, one round of loads in flight, then a shuffle-OR), 1024 / P words per pass; the ranks by a wave
-// scan + a scan of the 16 wave sums.
-template <int P>
-__global__ __launch_bounds__(1024) void outlier_index_kernel(const uint32_t *__restrict__ partial, int nchunks,
-                                                             int nwords, uint32_t *__restrict__ bits,
-                                                             int *__restrict__ rank, int *__restrict__ idx) {
-    __shared__ int wsum[16];
-    __shared__ int base;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int s = tid % P;
-    if (tid == 0) base = 0;
+    if ((tid & 7) == 0 && w < nwords)
+        __hip_atomic_store(partial + (int64_t)blockIdx.y * nwords + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int w0 = 0; w0 < nwords; w0 += 1024 / P) {
-        const int w = w0 + tid / P;
-        uint32_t word = 0;
-        if (w < nwords) {
-            int ch = s;
-            for (; ch + 7 * P < nchunks; ch += 8 * P) {  // 8 loads in flight per thread
-                uint32_t u[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) u[e] = partial[(int64_t)(ch + e * P) * nwords + w];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) word |= u[e];
-            }
-            for (; ch < nchunks; ch += P) word |= partial[(int64_t)ch * nwords + w];
-        }
-#pragma unroll
-        for (int off = 1; off < P; off <<= 1) word |= (uint32_t)__shfl_xor((int)word, off, 64);
-        const int pc = (s == 0 && w < nwords) ? __popc(word) : 0;
-        int x = pc;  // inclusive scan over the block in thread order (= word order)
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(x, off, 64);
-            if (lane >= off) x += v;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        int before = base;
-        for (int j = 0; j < wave; ++j) before += wsum[j];
-        const int below = before + x - pc;
-        if (s == 0 && w < nwords) {
-            bits[w] = word;
-            rank[w] = below;
-            int j = 0;
-            for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int tot = 0;
-            for (int j = 0; j < 16; ++j) tot += wsum[j];
-            base += tot;
-        }
-        __syncthreads();
+    const unsigned total = gridDim.x * gridDim.y;
+    if (tid == 0) {
+        const unsigned a = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = a;
+        // every workgroup has arrived: nobody else touches the ticket in this launch
+        if (a == total - 1) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (tid == 0) idx[0] = base;
+    __syncthreads();
+    if (last != total - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the sc1 loads stay below
+    build_index<P>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count);
+    __syncthreads();
+    if (tid == 0) idx[0] = count;
 }
 
 __device__ __forceinline__ bool bit_of(const uint32_t *bits, int64_t c) { return (bits[c >> 5] >> (c & 31)) & 1u; }
@@ -194,18 +216,26 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
     return v;
 }
 
-// column mask, ranks, index list and count of X's outlier columns
-hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, hipStream_t s) {
+template <bool VEC>
+void launch_flags(const dim3 &grid, hipStream_t s, const float *X, int64_t xsh, int m, int k, float t,
+                  const OutlierScratch &v, unsigned *ticket) {
+    const int nw = v.nwords;
+    auto go = [&](auto kern) { kern<<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, nw, ticket, v.bits, v.rank, v.idx); };
+    if (nw <= 16) go(outlier_flags_kernel<VEC, 16>);
+    else if (nw <= 32) go(outlier_flags_kernel<VEC, 8>);
+    else if (nw <= 64) go(outlier_flags_kernel<VEC, 4>);
+    else if (nw <= 128) go(outlier_flags_kernel<VEC, 2>);
+    else go(outlier_flags_kernel<VEC, 1>);
+}
+
+// column mask, ranks, index list and count of X's outlier columns: ONE launch (the last flags workgroup
+// builds the index)
+hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, unsigned *ticket,
+                        hipStream_t s) {
     const dim3 grid((unsigned)((k + kFlagCols - 1) / kFlagCols), (unsigned)v.nchunks);
     const bool vec = (k % 4 == 0) && (xsh % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
-    if (vec) outlier_flags_kernel<true><<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords);
-    else outlier_flags_kernel<false><<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords);
-    const int nw = v.nwords;
-    if (nw <= 64) outlier_index_kernel<16><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
-    else if (nw <= 128) outlier_index_kernel<8><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
-    else if (nw <= 256) outlier_index_kernel<4><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
-    else if (nw <= 512) outlier_index_kernel<2><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
-    else outlier_index_kernel<1><<<1, 1024, 0, s>>>(v.partial, v.nchunks, nw, v.bits, v.rank, v.idx);
+    if (vec) launch_flags<true>(grid, s, X, xsh, m, k, t, v, ticket);
+    else launch_flags<false>(grid, s, X, xsh, m, k, t, v, ticket);
     return hipGetLastError();
 }
 
@@ -221,14 +251,14 @@ size_t outlier_scratch_bytes(int m, int n, int k) {
 // Fast path: flags + index, the masked single-pass pack, the 256-tile GEMM with the fp32 chain in its
 // epilogue.  hipErrorNotSupported (nothing launched) outside its envelope.
 hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
-                        PackedView va, PackedView vb, float range, hipStream_t s) {
+                        unsigned *ticket, PackedView va, PackedView vb, float range, hipStream_t s) {
     if (!gemm_outlier_ok(m, n, (int)va.k_pad) || !pack_single_pass_outlier_ok(X, k, m, k, W, n, n)) return hipErrorNotSupported;
     // xo / wo (offsets of a256 from the scratch) are read and written as float4: a scratch that is not 16-B
     // aligned takes the materialising fallback before anything is enqueued
     if (reinterpret_cast<uintptr_t>(scratch) % 16 != 0) return hipErrorNotSupported;
     const OutlierScratch v = scratch_view(scratch, m, k);
     const int64_t wo_ld = round_up(n, 256);
-    hipError_t e = outlier_scan(X, k, m, k, t, v, s);
+    hipError_t e = outlier_scan(X, k, m, k, t, v, ticket, s);
     if (e != hipSuccess) return e;
     e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, v.bits, v.rank, v.idx, v.xm, v.wm, wo_ld,
                                         s);
@@ -241,11 +271,11 @@ hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, 
 // Fallback phase 1: flags, indices, X', W' into scratch; the caller then runs the int8 chain on (X', W')
 // and phase 2 (outlier_finish) adds the fp32 outlier products.
 hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, float t,
-                           void *scratch, float **Xm, float **Wm, hipStream_t s) {
+                           void *scratch, unsigned *ticket, float **Xm, float **Wm, hipStream_t s) {
     const OutlierScratch v = scratch_view(scratch, m, k);
     *Xm = v.xm;
     *Wm = v.wm;
-    hipError_t e = outlier_scan(X, xsh, m, k, t, v, s);
+    hipError_t e = outlier_scan(X, xsh, m, k, t, v, ticket, s);
     if (e != hipSuccess) return e;
     outlier_mask_kernel<<<(unsigned)(m + k), 256, 0, s>>>(X, xsh, m, k, W, wsh, n, v.bits, v.xm, v.wm);
     return hipGetLastError();

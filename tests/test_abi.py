@@ -265,6 +265,7 @@ def _copy_tree(qg, dst):
     import shutil
     pkg = dst / "pkg"
     shutil.copytree(os.path.join(qg.PKG_DIR, "csrc"), pkg / "csrc")
+    shutil.copytree(os.path.join(qg.PKG_DIR, "src"), pkg / "src")
     shutil.copy(os.path.join(qg.PKG_DIR, "Makefile"), pkg / "Makefile")
     shutil.copy(os.path.join(qg.PKG_DIR, "__init__.py"), pkg / "__init__.py")
     shutil.copytree(os.path.join(REPO, "include"), dst / "include")
@@ -298,6 +299,7 @@ def test_stale_binary_is_rejected(qg, tmp_path):
         f.write("\n// edited after the build\n")
     stale = _load_copy(pkg, "qgemm_copy_stale")
     assert stale.source_hash() != qg.source_hash()
+    assert stale.file_hash() == qg.source_hash(), "the binary's own tag names the sources it was built from"
     with pytest.raises(RuntimeError, match="built from sources"):
         stale.check_binary()
 
