@@ -33,10 +33,10 @@ __global__ void put_outliers(float *X, int m, int k, int every, int ncols) {
 int main(int argc, char **argv) {
     const int m = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 4096, k = argc > 3 ? atoi(argv[3]) : 4096;
     const int rounds = argc > 4 ? atoi(argv[4]) : 9, reps = 10;
-    float *X, *W; void *PX, *PW, *scr; unsigned *ticket;
+    float *X, *W; void *PX, *PW, *scr;
     CK(hipMalloc(&X, (size_t)m * k * 4)); CK(hipMalloc(&W, (size_t)k * n * 4));
     CK(hipMalloc(&PX, packed_bytes(m, k))); CK(hipMalloc(&PW, packed_bytes(n, k)));
-    CK(hipMalloc(&scr, outlier_scratch_bytes(m, n, k))); CK(hipMalloc(&ticket, 256)); CK(hipMemset(ticket, 0, 256));
+    CK(hipMalloc(&scr, outlier_scratch_bytes(m, n, k)));
     CK(launch_fill_uniform(X, (int64_t)m * k, 11, -1.f, 1.f, nullptr));
     CK(launch_fill_uniform(W, (int64_t)k * n, 12, -1.f, 1.f, nullptr));
     put_outliers<<<dim3(8, (m / 50 + 255) / 256 + 1), 256>>>(X, m, k, 50, 8);
@@ -48,7 +48,7 @@ int main(int argc, char **argv) {
     const int g = nstrips + npad + nx;
     const int64_t wo_ld = round_up(n, 256);
     const float range = 127.f;
-    auto flags = [&](float t) { CK(outlier_scan(X, k, m, k, t, v, ticket, s0)); };
+    auto flags = [&](float t) { CK(outlier_scan(X, k, m, k, t, v, s0)); };
     const OutlierMask om{v.bits, v.rank, v.idx, v.xm, v.wm, wo_ld};
     auto pack = [&](int var) {
         if (var == 0)

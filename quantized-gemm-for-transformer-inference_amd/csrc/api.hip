@@ -69,8 +69,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Split-K scratch for qgemm_mm_packed (which has no workspace argument): grow-only, one per
 // (device, stream) -- the tickets and slabs are only safe to reuse in stream order.
-// never shared: split-K tickets and the outlier flags' arrival ticket must stay zero between calls
-enum ScratchUse { kScratchSplitK = 0, kScratchErrorStats = 1, kScratchOutlierTicket = 2 };
+enum ScratchUse { kScratchSplitK = 0, kScratchErrorStats = 1 };  // never shared: split-K tickets must stay zero
 struct ScratchKey {
     int dev;
     hipStream_t stream;
@@ -326,21 +325,16 @@ int qgemm_mm_outlier(const float *A, const float *B, float *C, int m, int n, int
     hipStream_t s = static_cast<hipStream_t>(stream);
     char *scratch = static_cast<char *>(workspace);
     char *ws2 = scratch + align256(outlier_scratch_bytes(m, n, k));
-    // the flags launch's arrival ticket: library-owned, zeroed once, one per (device, stream), re-zeroed by the
-    // workgroup that arrives last (a caller's workspace may hold anything on its first use)
-    void *tk = nullptr;
-    if (const hipError_t e = cached_scratch(256, s, kScratchOutlierTicket, &tk); e != hipSuccess) return err(e);
-    unsigned *ticket = static_cast<unsigned *>(tk);
     {
         // fast path: the packed operands in the plain chain's slots of ws2 (no split-K: no tickets)
         char *pa = ws2 + align256(gemm_scratch_bytes(m, n, k));
         char *pb = pa + align256(packed_bytes(m, k));
-        const hipError_t e = outlier_fast(A, B, C, m, n, k, threshold, scratch, ticket, packed_view(pa, m, k),
+        const hipError_t e = outlier_fast(A, B, C, m, n, k, threshold, scratch, packed_view(pa, m, k),
                                           packed_view(pb, n, k), kDefaultRange, s);
         if (e != hipErrorNotSupported) return err(e);
     }
     float *Xm = nullptr, *Wm = nullptr;
-    hipError_t e = outlier_prepare(A, k, B, n, m, n, k, threshold, scratch, ticket, &Xm, &Wm, s);
+    hipError_t e = outlier_prepare(A, k, B, n, m, n, k, threshold, scratch, &Xm, &Wm, s);
     if (e != hipSuccess) return err(e);
     // the int8 part on the outlier-free operands (their scales no longer see the outliers)
     const int rc = op_mm_quantize_ws(Xm, k, 1, Wm, n, 1, C, n, 1, m, n, k, kDefaultRange, ws2,

@@ -19,10 +19,18 @@
 // Other shapes: flags + index, X'/W' materialised by a masking pass, the plain drop-in on them, and a
 // correction kernel adding the chain to O.
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "qgemm_internal.h"
 
 namespace qgemm {
+
+// The flags launch's arrival tickets: a zero-initialised array of the code object (per device), one 128-B line per
+// slot, one slot per stream (outlier_ticket_slot).  Each launch's last workgroup re-zeroes its slot, so a slot is 0
+// between calls -- without any allocation or memset, so the first call on a stream may be inside a graph capture.
+constexpr int kTicketSlots = 1024, kTicketStride = 32;
+__device__ unsigned g_flags_ticket[kTicketSlots * kTicketStride];
 
 namespace {
 
@@ -94,13 +102,14 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
 // [64 chunk, 64 chunk + 64).  Thread t: columns 1024 bx + 4t .. +3.  Then the workgroup that arrives last
 // (one agent-scope add per workgroup on *ticket, after every wave's sc1 partial stores have drained: the
 // write-through hand-off of MI355X_MICROARCH.md, row 1) builds the column mask, ranks, list and count
-// (build_index) and re-zeroes the ticket for the next call -- no separate index launch.  *ticket is
-// library-owned, zeroed once at allocation, one per (device, stream).
+// (build_index) and re-zeroes the ticket for the next call -- no separate index launch.  The ticket is the
+// stream's slot of g_flags_ticket.
 template <bool VEC, int P>
 __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
                                                             float t, uint32_t *__restrict__ partial, int nwords,
-                                                            unsigned *__restrict__ ticket, uint32_t *__restrict__ bits,
+                                                            int slot, uint32_t *__restrict__ bits,
                                                             int *__restrict__ rank, int *__restrict__ idx) {
+    unsigned *ticket = g_flags_ticket + slot * kTicketStride;
     __shared__ int wsum[4];
     __shared__ unsigned last;
     __shared__ int count;
@@ -186,6 +195,19 @@ __global__ __launch_bounds__(256) void outlier_mm_kernel(const float *__restrict
     O[(int64_t)i * osh + j] = __fadd_rn(O[(int64_t)i * osh + j], acc);
 }
 
+// the stream's ticket slot (host bookkeeping only: no HIP call, so it is capture-safe); -1 when all are taken
+int outlier_ticket_slot(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<hipStream_t, int> slots;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = slots.find(s);
+    if (it != slots.end()) return it->second;
+    if ((int)slots.size() >= kTicketSlots) return -1;
+    const int id = (int)slots.size();
+    slots.emplace(s, id);
+    return id;
+}
+
 struct OutlierScratch {
     uint32_t *partial, *bits;
     int *rank, *idx;  // idx[0] = count
@@ -218,9 +240,9 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
 
 template <bool VEC>
 void launch_flags(const dim3 &grid, hipStream_t s, const float *X, int64_t xsh, int m, int k, float t,
-                  const OutlierScratch &v, unsigned *ticket) {
+                  const OutlierScratch &v, int slot) {
     const int nw = v.nwords;
-    auto go = [&](auto kern) { kern<<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, nw, ticket, v.bits, v.rank, v.idx); };
+    auto go = [&](auto kern) { kern<<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, nw, slot, v.bits, v.rank, v.idx); };
     if (nw <= 16) go(outlier_flags_kernel<VEC, 16>);
     else if (nw <= 32) go(outlier_flags_kernel<VEC, 8>);
     else if (nw <= 64) go(outlier_flags_kernel<VEC, 4>);
@@ -230,12 +252,13 @@ void launch_flags(const dim3 &grid, hipStream_t s, const float *X, int64_t xsh, 
 
 // column mask, ranks, index list and count of X's outlier columns: ONE launch (the last flags workgroup
 // builds the index)
-hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, unsigned *ticket,
-                        hipStream_t s) {
+hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, hipStream_t s) {
+    const int slot = outlier_ticket_slot(s);
+    if (slot < 0) return hipErrorOutOfMemory;  // more streams than ticket slots
     const dim3 grid((unsigned)((k + kFlagCols - 1) / kFlagCols), (unsigned)v.nchunks);
     const bool vec = (k % 4 == 0) && (xsh % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
-    if (vec) launch_flags<true>(grid, s, X, xsh, m, k, t, v, ticket);
-    else launch_flags<false>(grid, s, X, xsh, m, k, t, v, ticket);
+    if (vec) launch_flags<true>(grid, s, X, xsh, m, k, t, v, slot);
+    else launch_flags<false>(grid, s, X, xsh, m, k, t, v, slot);
     return hipGetLastError();
 }
 
@@ -251,14 +274,14 @@ size_t outlier_scratch_bytes(int m, int n, int k) {
 // Fast path: flags + index, the masked single-pass pack, the 256-tile GEMM with the fp32 chain in its
 // epilogue.  hipErrorNotSupported (nothing launched) outside its envelope.
 hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
-                        unsigned *ticket, PackedView va, PackedView vb, float range, hipStream_t s) {
+                        PackedView va, PackedView vb, float range, hipStream_t s) {
     if (!gemm_outlier_ok(m, n, (int)va.k_pad) || !pack_single_pass_outlier_ok(X, k, m, k, W, n, n)) return hipErrorNotSupported;
     // xo / wo (offsets of a256 from the scratch) are read and written as float4: a scratch that is not 16-B
     // aligned takes the materialising fallback before anything is enqueued
     if (reinterpret_cast<uintptr_t>(scratch) % 16 != 0) return hipErrorNotSupported;
     const OutlierScratch v = scratch_view(scratch, m, k);
     const int64_t wo_ld = round_up(n, 256);
-    hipError_t e = outlier_scan(X, k, m, k, t, v, ticket, s);
+    hipError_t e = outlier_scan(X, k, m, k, t, v, s);
     if (e != hipSuccess) return e;
     e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, v.bits, v.rank, v.idx, v.xm, v.wm, wo_ld,
                                         s);
@@ -271,11 +294,11 @@ hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, 
 // Fallback phase 1: flags, indices, X', W' into scratch; the caller then runs the int8 chain on (X', W')
 // and phase 2 (outlier_finish) adds the fp32 outlier products.
 hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, float t,
-                           void *scratch, unsigned *ticket, float **Xm, float **Wm, hipStream_t s) {
+                           void *scratch, float **Xm, float **Wm, hipStream_t s) {
     const OutlierScratch v = scratch_view(scratch, m, k);
     *Xm = v.xm;
     *Wm = v.wm;
-    hipError_t e = outlier_scan(X, xsh, m, k, t, v, ticket, s);
+    hipError_t e = outlier_scan(X, xsh, m, k, t, v, s);
     if (e != hipSuccess) return e;
     outlier_mask_kernel<<<(unsigned)(m + k), 256, 0, s>>>(X, xsh, m, k, W, wsh, n, v.bits, v.xm, v.wm);
     return hipGetLastError();

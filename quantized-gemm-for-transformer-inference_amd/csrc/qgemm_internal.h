@@ -196,17 +196,15 @@ hipError_t launch_add_layernorm_rows_pack(const float *A, const float *B, float 
                                           PackedView out, hipStream_t stream);
 // LLM.int8() outlier decomposition (outlier.hip).
 size_t outlier_scratch_bytes(int m, int n, int k);
-// `ticket`: one zeroed word owned by the library per (device, stream) (api.hip kScratchOutlierTicket); the flags
-// launch's last workgroup builds the column index and re-zeroes it
 hipError_t outlier_prepare(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, float t,
-                           void *scratch, unsigned *ticket, float **Xm, float **Wm, hipStream_t s);
+                           void *scratch, float **Xm, float **Wm, hipStream_t s);
 hipError_t outlier_finish(const float *X, int64_t xsh, const float *W, int64_t wsh, int m, int n, int k, void *scratch,
                           float *O, int64_t osh, hipStream_t s);
 int outlier_count_slot(int k, const void *scratch, int *count_host);
 // fast path (flags, indices, masked single-pass pack, GEMM with the fp32 chain in its epilogue) into the
 // packed views va / vb; hipErrorNotSupported (nothing launched) outside its envelope (row-major operands)
 hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
-                        unsigned *ticket, PackedView va, PackedView vb, float range, hipStream_t s);
+                        PackedView va, PackedView vb, float range, hipStream_t s);
 // The encoder counterpart (encoder.hip).
 struct Encoder;
 uint64_t encoder_weight_seed(uint64_t base, int block, int kind, int head);

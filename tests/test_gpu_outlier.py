@@ -131,10 +131,11 @@ def test_decomposition_reduces_quantization_error(qg, oracle, device):
 
 
 def test_outlier_graph_capture_and_repeat(qg, oracle, device):
-    """qgemm_mm_outlier makes no allocation and no host sync (the outlier count stays on the device), so the
-    four fast-path launches (flags, index, masked pack, GEMM with the chain) can be captured in a HIP graph
-    and replayed; and 20 eager calls on one workspace give the same bits every time (race screen of the
-    partial-mask / rank / compact-value hand-offs)."""
+    """qgemm_mm_outlier makes no allocation and no host sync (the outlier count stays on the device; the flags
+    launch's arrival ticket is a zero-initialised slot of the code object), so the three fast-path launches
+    (flags with the last-arriver index, masked pack, GEMM with the chain) can be captured in a HIP graph --
+    here as the FIRST call on its stream -- and replayed; and 20 eager calls on one workspace give the same
+    bits every time (race screen of the partial-mask / last-arriver / rank / compact-value hand-offs)."""
     import torch
     M, N, K = 2560, 4096, 512
     X, W = _with_outliers(oracle, M, N, K, [0, 5, 77, 300, 511], 12)
