@@ -114,6 +114,40 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
+    if (only && std::string(only) == "spread") {
+        // round 5: attribute the block-end spread of the product kernel's store tail.  After 2 s of
+        // back-to-back launches, one stamped launch: per block its XCD, tile (tm, tn) as gemm_i8_f4 maps it, and the
+        // realtime stamps (us from the first start) of its start, loop end and end.  rows `blk,...` for offline analysis
+        unsigned long long *w4_sym;
+        CK(hipGetSymbolAddress((void **)&w4_sym, HIP_SYMBOL(g_w4_stamp)));
+        const int nb = p.tiles_m * p.tiles_n;
+        for (int rep = 0; rep < 3; ++rep) {
+            hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
+            float ms = 0;
+            CK(hipEventRecord(a));
+            while (ms < 2000) {
+                for (int i = 0; i < 200; ++i) gemm_i8_f4<kW4Stamp><<<grid, 256>>>(pf);
+                CK(hipEventRecord(z)); CK(hipEventSynchronize(z)); CK(hipEventElapsedTime(&ms, a, z));
+            }
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned long long> st((size_t)4096 * 6);
+            CK(hipMemcpy(st.data(), w4_sym, st.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long s0 = ~0ull;
+            for (int i = 0; i < nb; ++i) s0 = std::min(s0, st[(size_t)i * 6 + 1]);
+            for (int i = 0; i < nb; ++i) {
+                const unsigned long long *q = &st[(size_t)i * 6];
+                // gemm_i8_f4's map: xcd_remap, then group_tiles (kGroupM 4)
+                const int xcd = i & 7, q8 = nb >> 3, r8 = nb & 7;
+                const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (i >> 3);
+                const int per_group = 4 * p.tiles_n, grp = wid / per_group, first_m = grp * 4;
+                const int gsz = std::min(p.tiles_m - first_m, 4), w = wid - grp * per_group;
+                const int tm = first_m + w % gsz, tn = w / gsz;
+                printf("blk,%d,%d,%d,%d,%d,%.2f,%.2f,%.2f,%.4f\n", rep, i, xcd, tm, tn, (q[1] - s0) * 0.01,
+                       (q[3] - s0) * 0.01, (q[5] - s0) * 0.01, (double)(q[4] - q[2]) / std::max(1.0, (double)(q[5] - q[3])) * 0.1);
+            }
+        }
+        return 0;
+    }
     if (only && std::string(only) == "clock") {
         struct SV { const char *name; KernelFn fn; int threads; unsigned long long *sym; };
         unsigned long long *pp_sym, *w4_sym;

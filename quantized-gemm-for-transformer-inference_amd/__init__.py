@@ -374,7 +374,8 @@ def source_hash() -> str:
     import glob
     import hashlib
     rel = ["Makefile"]
-    for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.cpp", "../include/*.h", "src/*.cpp", "src/*/*.h", "src/*/*.cuh"):
+    for pat in ("csrc/*.hip", "csrc/*.h", "csrc/*.cpp", "../include/*.h", "src/*.cpp", "src/*.hip", "src/*/*.h",
+                "src/*/*.cuh"):
         rel += [os.path.relpath(p, PKG_DIR) for p in glob.glob(os.path.join(PKG_DIR, pat))]
     h = hashlib.sha256()
     for r in sorted(rel):

@@ -5,6 +5,7 @@ oracle (tests only) or the committed fixtures.  Bar: O, Xq, Wq, Acc bit-identica
 value-identical (their zero sign never reaches O: fl(Cx*Cw)+0 is +0 either way).
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -247,7 +248,8 @@ def test_256_tile_split_k_ticket_first_repeat(qg, oracle, device, M, N, K):
     """Race screen of the ticket-first split-K hand-off (gemm_i8_fm<kSplitFirst>): 20 back-to-back calls on the
     library scratch (each second arriver polls for the first's publish, then resets the ticket for the next
     launch), every output bit of every call.  The slices of a tile finish within a few microseconds of each
-    other, so both arrival orders occur; K = 2048 makes the two slices nearly equal (15 and 17 sub-steps)."""
+    other; K = 2048 makes the two slices nearly equal (15 and 17 sub-steps).  Slice 0 usually arrives first
+    here; the reverse order (slice 1 publishes while slice 0 waits) is forced by test_split_k_both_arrival_orders."""
     L = qg.load()
     assert L.qgemm_gemm_plan(M, N, K, None, None) == 2
     X, W = oracle.inputs(M, N, K, 57)
@@ -259,6 +261,21 @@ def test_256_tile_split_k_ticket_first_repeat(qg, oracle, device, M, N, K):
     torch.cuda.synchronize()
     for i, O in enumerate(outs):
         assert_bits_equal(O.cpu().numpy(), want, f"{M}x{N}x{K} repeat {i}")
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 4096, 2048), (2048, 4096, 16384)])
+def test_split_k_both_arrival_orders(qg, device, M, N, K):
+    """The ticket-first hand-off with the K split skewed both ways (build/splitk_order_check: the product kernel
+    instantiated with slice 0 = 8/64 of K -- slice 0 publishes -- 31/64 -- the product -- and 56/64 -- slice 1
+    finishes first and publishes while slice 0 spins), 20 calls each on one reused scratch: every output bit
+    equals the unsplit kernel's, and every ticket is back to 0."""
+    import json
+    import subprocess
+    exe = os.path.join(qg.PKG_DIR, "build", "splitk_order_check")
+    r = subprocess.run([exe, str(M), str(N), str(K), "20"], capture_output=True, text=True, timeout=120)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["ok"], out
+    assert [v["first64"] for v in out["variants"]] == [8, 31, 56]
 
 
 def test_device_generator_matches_oracle(qg, oracle, device):
