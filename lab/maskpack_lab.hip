@@ -22,6 +22,15 @@
 using namespace qgemm;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
+__global__ void sweep_kernel(const float *X, int64_t n4, uint32_t *sink) {
+    float a = 0.f;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 x = reinterpret_cast<const float4 *>(X)[i];
+        a += x.x + x.y + x.z + x.w;
+    }
+    if (a == 12345.f) sink[0] = 1u;  // keeps the loads
+}
+
 __global__ void put_outliers(float *X, int m, int k, int every, int ncols) {
     // ncols columns spread over k (bench.py outlier_columns), every `every`-th row |x| = 30
     const int c = blockIdx.x, i = threadIdx.x + blockIdx.y * 256;
@@ -37,6 +46,8 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&X, (size_t)m * k * 4)); CK(hipMalloc(&W, (size_t)k * n * 4));
     CK(hipMalloc(&PX, packed_bytes(m, k))); CK(hipMalloc(&PW, packed_bytes(n, k)));
     CK(hipMalloc(&scr, outlier_scratch_bytes(m, n, k)));
+    void *scr2;  // a second scratch: flags runs on it while the pack reads the first one's (unchanged) mask
+    CK(hipMalloc(&scr2, outlier_scratch_bytes(m, n, k)));
     CK(launch_fill_uniform(X, (int64_t)m * k, 11, -1.f, 1.f, nullptr));
     CK(launch_fill_uniform(W, (int64_t)k * n, 12, -1.f, 1.f, nullptr));
     put_outliers<<<dim3(8, (m / 50 + 255) / 256 + 1), 256>>>(X, m, k, 50, 8);
@@ -48,7 +59,14 @@ int main(int argc, char **argv) {
     const int g = nstrips + npad + nx;
     const int64_t wo_ld = round_up(n, 256);
     const float range = 127.f;
-    auto flags = [&](float t) { CK(outlier_scan(X, k, m, k, t, v, s0)); };
+    const OutlierScratch v2 = scratch_view(scr2, m, k);
+    // mode 0: flags into the pack's scratch; 1: flags into scratch2 (the pack's mask words were written long ago);
+    // 2: a plain read sweep of X instead of flags
+    auto flags = [&](float t, int mode = 0) {
+        if (mode == 0) CK(outlier_scan(X, k, m, k, t, v, s0));
+        else if (mode == 1) CK(outlier_scan(X, k, m, k, t, v2, s0));
+        else sweep_kernel<<<1024, 256, 0, s0>>>(X, (int64_t)m * k / 4, v2.partial);
+    };
     const OutlierMask om{v.bits, v.rank, v.idx, v.xm, v.wm, wo_ld};
     auto pack = [&](int var) {
         if (var == 0)
@@ -63,9 +81,10 @@ int main(int argc, char **argv) {
                                                                  n, vw.scale, vw.q, vw.rows_pad, nstrips, range, nullptr,
                                                                  0, om);
     };
-    struct V { std::string name; int pack; float t; bool with_flags; };
-    std::vector<V> vs = {{"plain", 0, 6.f, true}, {"mask", 1, 6.f, true}, {"mask5", 2, 6.f, true},
-                         {"mask0", 1, 1e30f, true}, {"plain_alone", 0, 6.f, false}, {"mask_alone", 1, 6.f, false}};
+    struct V { std::string name; int pack; float t; bool with_flags; int fmode; };
+    std::vector<V> vs = {{"plain", 0, 6.f, true, 0}, {"mask", 1, 6.f, true, 0}, {"mask5", 2, 6.f, true, 0},
+                         {"mask0", 1, 1e30f, true, 0}, {"plain_alone", 0, 6.f, false, 0}, {"mask_alone", 1, 6.f, false, 0},
+                         {"mask_flags2", 1, 6.f, true, 1}, {"mask_sweep", 1, 6.f, true, 2}, {"plain_sweep", 0, 6.f, true, 2}};
     // bit check: mask vs mask5
     std::vector<int8_t> a(vx.rows_pad * vx.k_pad), b(a.size());
     flags(6.f); pack(1); CK(hipStreamSynchronize(s0));
@@ -82,11 +101,12 @@ int main(int argc, char **argv) {
     for (int r = 0; r < rounds; ++r)
         for (size_t i = 0; i < vs.size(); ++i) {
             const V &x = vs[i];
-            for (int w = 0; w < 3; ++w) { if (x.with_flags) flags(x.t); pack(x.pack); }
+            flags(x.t, 0);  // the pack's own mask current for this variant's threshold (alone / flags2 / sweep reuse it)
+            for (int w = 0; w < 3; ++w) { if (x.with_flags) flags(x.t, x.fmode); pack(x.pack); }
             float af = 0, ap = 0;
             for (int j = 0; j < reps; ++j) {
                 CK(hipEventRecord(ev[0], s0));
-                if (x.with_flags) flags(x.t);
+                if (x.with_flags) flags(x.t, x.fmode);
                 CK(hipEventRecord(ev[1], s0));
                 pack(x.pack);
                 CK(hipEventRecord(ev[2], s0));

@@ -2,7 +2,7 @@
 # A/B of environment-selected variants on the C2 bench, interleaved: VARS="NAME=VAL ..." (one per variant,
 # "-" = default), REPS rounds.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/ab; mkdir -p $OUT
 CFG=${CFG:-c2}

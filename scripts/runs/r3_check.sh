@@ -2,7 +2,7 @@
 # Round-3 GPU session: parity tests, ping-pong staging A/B in the lab, a short bench.  Each GPU step has its
 # own time limit; a fault / abort / timeout ends the script (test failures, rc 1, do not).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3: gemm_i8_fm split-K (product) vs the ping-pong split-K kernel at FFN down, then the GPU tests.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/split; mkdir -p $OUT
 run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?
