@@ -29,12 +29,18 @@ namespace qgemm {
 // The flags launch's arrival tickets: a zero-initialised array of the code object (per device), one 128-B line per
 // slot, one slot per stream (outlier_ticket_slot).  Each launch's last workgroup re-zeroes its slot, so a slot is 0
 // between calls -- without any allocation or memset, so the first call on a stream may be inside a graph capture.
-constexpr int kTicketSlots = 1024, kTicketStride = 32;
+constexpr int kTicketSlots = 256, kTicketStride = 32;
 __device__ unsigned g_flags_ticket[kTicketSlots * kTicketStride];
+// K <= 32 768 (kAccWords words of 32 columns): each flags workgroup ORs its nonzero mask words into the slot's
+// accumulator with agent-scope atomics (performed at the memory side, coherent across XCDs), so the last workgroup
+// reads nwords words instead of every chunk's partial words; it re-zeroes them for the next call.
+constexpr int kAccWords = 1024;
+__device__ uint32_t g_flags_acc[kTicketSlots * kAccWords];
 
 namespace {
 
-constexpr int kChunkRows = 64;     // rows per flags block
+constexpr int kChunkRows = 64;     // rows per flags block (partial-word path, K > 32 768)
+constexpr int kAccChunkRows = 16;  // rows per flags block (accumulator path): 4x the workgroups in flight
 constexpr int kFlagCols = 1024;    // columns per flags block (256 threads x 4)
 
 // AbsCompareLTEConstFunc (op_elemwise.cuh:296-304): 0 when a in [-b, b], else 1 (NaN -> 1)
@@ -98,24 +104,26 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
     if (tid == 0) *base = run;
 }
 
-// partial[chunk][word]: bit c of word w set when column 32w + c holds an outlier in rows
-// [64 chunk, 64 chunk + 64).  Thread t: columns 1024 bx + 4t .. +3.  Then the workgroup that arrives last
-// (one agent-scope add per workgroup on *ticket, after every wave's sc1 partial stores have drained: the
-// write-through hand-off of MI355X_MICROARCH.md, row 1) builds the column mask, ranks, list and count
-// (build_index) and re-zeroes the ticket for the next call -- no separate index launch.  The ticket is the
-// stream's slot of g_flags_ticket.
-template <bool VEC, int P>
+// Mask word w of a row chunk: bit c set when column 32w + c holds an outlier in the chunk's rows.  Thread t: columns
+// 1024 bx + 4t .. +3 over `rows` rows from blockIdx.y * rows.  kAcc: nonzero words are ORed into the stream's
+// accumulator g_flags_acc (agent-scope atomics); else every word is stored to partial[chunk][word] (sc1).  Then each
+// workgroup, after every wave's stores / atomics have drained, adds 1 to the stream's ticket (one lane, agent scope:
+// the write-through hand-off of MI355X_MICROARCH.md, sc1 table row 1); the workgroup whose add returns the last
+// value builds the column mask, ranks, list and count (build_index over the accumulator or the partial words) and
+// re-zeroes the ticket and the accumulator for the next call -- no separate index launch.
+template <bool VEC, int P, bool kAcc>
 __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
-                                                            float t, uint32_t *__restrict__ partial, int nwords,
-                                                            int slot, uint32_t *__restrict__ bits,
+                                                            float t, int rows, uint32_t *__restrict__ partial,
+                                                            int nwords, int slot, uint32_t *__restrict__ bits,
                                                             int *__restrict__ rank, int *__restrict__ idx) {
     unsigned *ticket = g_flags_ticket + slot * kTicketStride;
+    uint32_t *acc = g_flags_acc + slot * kAccWords;
     __shared__ int wsum[4];
     __shared__ unsigned last;
     __shared__ int count;
     const int tid = threadIdx.x;
     const int c = blockIdx.x * kFlagCols + 4 * tid;
-    const int r0 = blockIdx.y * kChunkRows, r1 = min(m, r0 + kChunkRows);
+    const int r0 = blockIdx.y * rows, r1 = min(m, r0 + rows);
     uint32_t nib = 0;
     if (c < k) {
         if constexpr (VEC) {
@@ -139,8 +147,14 @@ __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restr
     word |= __shfl_xor(word, 2, 64);
     word |= __shfl_xor(word, 4, 64);
     const int w = blockIdx.x * (kFlagCols / 32) + (tid >> 3);
-    if ((tid & 7) == 0 && w < nwords)
-        __hip_atomic_store(partial + (int64_t)blockIdx.y * nwords + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((tid & 7) == 0 && w < nwords) {
+        if constexpr (kAcc) {
+            if (word) __hip_atomic_fetch_or(acc + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(partial + (int64_t)blockIdx.y * nwords + w, word, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const unsigned total = gridDim.x * gridDim.y;
@@ -153,9 +167,12 @@ __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restr
     __syncthreads();
     if (last != total - 1) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the sc1 loads stay below
-    build_index<P>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count);
-    __syncthreads();
+    if constexpr (kAcc) build_index<P>(acc, 1, nwords, bits, rank, idx, wsum, &count);
+    else build_index<P>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count);
+    __syncthreads();  // every accumulator word has been read
     if (tid == 0) idx[0] = count;
+    if constexpr (kAcc)
+        for (int i = tid; i < nwords; i += 256) __hip_atomic_store(acc + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ bool bit_of(const uint32_t *bits, int64_t c) { return (bits[c >> 5] >> (c & 31)) & 1u; }
@@ -239,15 +256,22 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
 }
 
 template <bool VEC>
-void launch_flags(const dim3 &grid, hipStream_t s, const float *X, int64_t xsh, int m, int k, float t,
-                  const OutlierScratch &v, int slot) {
+void launch_flags(hipStream_t s, const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v,
+                  int slot) {
     const int nw = v.nwords;
-    auto go = [&](auto kern) { kern<<<grid, 256, 0, s>>>(X, xsh, m, k, t, v.partial, nw, slot, v.bits, v.rank, v.idx); };
-    if (nw <= 16) go(outlier_flags_kernel<VEC, 16>);
-    else if (nw <= 32) go(outlier_flags_kernel<VEC, 8>);
-    else if (nw <= 64) go(outlier_flags_kernel<VEC, 4>);
-    else if (nw <= 128) go(outlier_flags_kernel<VEC, 2>);
-    else go(outlier_flags_kernel<VEC, 1>);
+    const unsigned gx = (unsigned)((k + kFlagCols - 1) / kFlagCols);
+    if (nw <= kAccWords) {
+        // the accumulator path: 16-row chunks (more workgroups in flight; the last one reads nw words, not chunks)
+        int rows = kAccChunkRows;
+        while ((m + rows - 1) / rows > 65535) rows *= 2;
+        const dim3 grid(gx, (unsigned)((m + rows - 1) / rows));
+        outlier_flags_kernel<VEC, 1, true><<<grid, 256, 0, s>>>(X, xsh, m, k, t, rows, v.partial, nw, slot, v.bits, v.rank,
+                                                                v.idx);
+        return;
+    }
+    // K > 32 768: 64-row chunks store their words; the last workgroup ORs every chunk's (one word per thread)
+    outlier_flags_kernel<VEC, 1, false><<<dim3(gx, (unsigned)v.nchunks), 256, 0, s>>>(X, xsh, m, k, t, kChunkRows, v.partial,
+                                                                                      nw, slot, v.bits, v.rank, v.idx);
 }
 
 // column mask, ranks, index list and count of X's outlier columns: ONE launch (the last flags workgroup
@@ -255,10 +279,10 @@ void launch_flags(const dim3 &grid, hipStream_t s, const float *X, int64_t xsh, 
 hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, hipStream_t s) {
     const int slot = outlier_ticket_slot(s);
     if (slot < 0) return hipErrorOutOfMemory;  // more streams than ticket slots
-    const dim3 grid((unsigned)((k + kFlagCols - 1) / kFlagCols), (unsigned)v.nchunks);
+    if (v.nchunks > 65535) return hipErrorNotSupported;
     const bool vec = (k % 4 == 0) && (xsh % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
-    if (vec) launch_flags<true>(grid, s, X, xsh, m, k, t, v, slot);
-    else launch_flags<false>(grid, s, X, xsh, m, k, t, v, slot);
+    if (vec) launch_flags<true>(s, X, xsh, m, k, t, v, slot);
+    else launch_flags<false>(s, X, xsh, m, k, t, v, slot);
     return hipGetLastError();
 }
 

@@ -14,5 +14,5 @@ timeout -k 10 300 python bench.py --config c2_outlier --no-cpu-baseline --cold-s
 grep -o '"value": [0-9.]*' $out/bench_c2_outlier_$i.log | head -1
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --config c2_outlier --no-cpu-baseline --cold-steps 0 --no-error-stats --steps 50 > $GRAFT_REPO_ROOT/$out/prof.log 2>&1 || { tail $GRAFT_REPO_ROOT/$out/prof.log; exit 1; }
-find $GRAFT_REPO_ROOT/$out/prof -name "*kernel_stats.csv" | head -1 | xargs cat | cut -c1-200 | head -12
+python3 $GRAFT_REPO_ROOT/scripts/rocpd_top.py $GRAFT_REPO_ROOT/$out/prof/run_results.db | tee $GRAFT_REPO_ROOT/$out/kernel_stats.txt
 echo done

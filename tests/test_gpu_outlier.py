@@ -27,8 +27,9 @@ def _with_outliers(oracle, M, N, K, cols, seed):
     return X.astype(np.float32), W
 
 
+# (72, 40, 33000): K > 32 768 = past the flags launch's accumulator -- its partial-word path, 64-row chunks
 @pytest.mark.parametrize("M,N,K,cols", [(300, 200, 512, [3, 77, 400]), (2048, 1024, 4096, list(range(5, 4096, 257))),
-                                        (64, 96, 130, [0, 129])])
+                                        (64, 96, 130, [0, 129]), (72, 40, 33000, [0, 31, 32767, 32768, 32999])])
 def test_outlier_decomposition_bit_exact(qg, oracle, device, M, N, K, cols):
     X, W = _with_outliers(oracle, M, N, K, cols, 5)
     C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
@@ -51,10 +52,9 @@ def test_outlier_fast_path_bit_exact(qg, oracle, device, M, N, K, cols):
     assert_bits_equal(C.cpu().numpy(), want, f"outlier fast path {M}x{N}x{K}")
 
 
-# the fast path at 128 and 129 flag chunks of 64 rows (the index launch ORs every chunk word; a round-4 variant that
-# folded that OR into the pack below 129 chunks, lab/outlier_fold_experiment.patch, was tested here), counts read
-# back from the workspace
-@pytest.mark.parametrize("M,N,K,cols", [(8192, 1280, 128, [0, 31, 32, 127]), (8256, 1280, 256, [1, 64, 200, 255])])
+# the fast path with many flag workgroups (16-row chunks since round 5: 512 / 516 chunks; M = 8257 also leaves a
+# partial last chunk), counts read back from the workspace
+@pytest.mark.parametrize("M,N,K,cols", [(8192, 1280, 128, [0, 31, 32, 127]), (8257, 1280, 256, [1, 64, 200, 255])])
 def test_outlier_fast_path_many_chunks(qg, oracle, device, M, N, K, cols):
     X, W = _with_outliers(oracle, M, N, K, cols, 13)
     C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
