@@ -39,8 +39,7 @@ __device__ uint32_t g_flags_acc[kTicketSlots * kAccWords];
 
 namespace {
 
-constexpr int kChunkRows = 64;     // rows per flags block (partial-word path, K > 32 768)
-constexpr int kAccChunkRows = 16;  // rows per flags block (accumulator path): 4x the workgroups in flight
+constexpr int kChunkRows = 64;     // rows per flags block
 constexpr int kFlagCols = 1024;    // columns per flags block (256 threads x 4)
 
 // AbsCompareLTEConstFunc (op_elemwise.cuh:296-304): 0 when a in [-b, b], else 1 (NaN -> 1)
@@ -51,12 +50,12 @@ __device__ __forceinline__ bool is_outlier(float a, float b) {
 // bits[w] = OR of the chunk masks, rank[w] = set bits below word w, idx[1 + ...] = the outlier columns in
 // ascending order, idx[0] = their count -- by the ONE workgroup of outlier_flags_kernel that arrives last.  P
 // adjacent threads share a word (each ORs every P-th chunk, 16 sc1 loads in flight, then a shuffle-OR),
-// kThreads / P words per pass; the ranks by a wave scan + a scan of the 4 wave sums.
-template <int P>
+// kThreads / P words per pass; the ranks by a wave scan + a scan of the wave sums.
+template <int P, int kThreads>
 __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial, int nchunks, int nwords,
                                             uint32_t *__restrict__ bits, int *__restrict__ rank, int *__restrict__ idx,
                                             int *wsum, int *base) {
-    constexpr int kThreads = 256;
+    constexpr int kWaves = kThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s = tid % P;
     int run = 0;  // count of outlier columns in the words already done (the same in every thread)
@@ -98,32 +97,38 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
             int j = 0;
             for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
         }
-        run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+        for (int j = 0; j < kWaves; ++j) run += wsum[j];
         __syncthreads();  // wsum is rewritten by the next pass
     }
     if (tid == 0) *base = run;
 }
 
-// Mask word w of a row chunk: bit c set when column 32w + c holds an outlier in the chunk's rows.  Thread t: columns
-// 1024 bx + 4t .. +3 over `rows` rows from blockIdx.y * rows.  kAcc: nonzero words are ORed into the stream's
-// accumulator g_flags_acc (agent-scope atomics); else every word is stored to partial[chunk][word] (sc1).  Then each
-// workgroup, after every wave's stores / atomics have drained, adds 1 to the stream's ticket (one lane, agent scope:
-// the write-through hand-off of MI355X_MICROARCH.md, sc1 table row 1); the workgroup whose add returns the last
-// value builds the column mask, ranks, list and count (build_index over the accumulator or the partial words) and
-// re-zeroes the ticket and the accumulator for the next call -- no separate index launch.
-template <bool VEC, int P, bool kAcc>
-__global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
-                                                            float t, int rows, uint32_t *__restrict__ partial,
-                                                            int nwords, int slot, uint32_t *__restrict__ bits,
-                                                            int *__restrict__ rank, int *__restrict__ idx) {
-    unsigned *ticket = g_flags_ticket + slot * kTicketStride;
+// Mask word w of a 64-row chunk: bit c set when column 32w + c holds an outlier in the chunk's rows.  1024 threads =
+// 4 row groups x 256 column threads: thread (g, t) reads columns 1024 bx + 4t .. +3 of rows 16 g .. 16 g + 15 of
+// the chunk (16 float4 loads in flight per thread, 16 waves per CU), the groups' nibbles meet in LDS.  kAcc:
+// nonzero words are ORed into the stream's accumulator g_flags_acc (agent-scope atomics); else every word is stored
+// to partial[chunk][word] (sc1).  Then each workgroup, after every wave's stores / atomics have drained, arrives
+// on its XCD's counter of the stream's ticket slot (one lane, agent scope), and the last of each XCD on the slot's
+// global counter -- sharded, because ≈ 12 ns per arrival serialise on one counter (MI355X_MICROARCH.md fan-in row);
+// the write-through hand-off of the sc1 table, row 1, at each level.  The workgroup that arrives last overall
+// builds the column mask, ranks, list and count (build_index over the accumulator or the partial words) and
+// re-zeroes the counters and the accumulator for the next call -- no separate index launch.
+constexpr int kFlagThreads = 1024, kFlagGroups = 4, kGroupRows = kChunkRows / kFlagGroups;
+template <bool VEC, bool kAcc>
+__global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m,
+                                                                     int k, float t, uint32_t *__restrict__ partial,
+                                                                     int nwords, int slot, uint32_t *__restrict__ bits,
+                                                                     int *__restrict__ rank, int *__restrict__ idx) {
+    unsigned *ticket = g_flags_ticket + slot * kTicketStride;  // [0..7]: per-XCD counters, [16]: the global one
     uint32_t *acc = g_flags_acc + slot * kAccWords;
-    __shared__ int wsum[4];
+    __shared__ int wsum[kFlagThreads / 64];
+    __shared__ uint32_t nibs[kFlagGroups - 1][256];
     __shared__ unsigned last;
     __shared__ int count;
-    const int tid = threadIdx.x;
-    const int c = blockIdx.x * kFlagCols + 4 * tid;
-    const int r0 = blockIdx.y * rows, r1 = min(m, r0 + rows);
+    const int tid = threadIdx.x, ct = tid & 255, g = tid >> 8;
+    const int c = blockIdx.x * kFlagCols + 4 * ct;
+    const int r0 = blockIdx.y * kChunkRows + g * kGroupRows, r1 = min(m, r0 + kGroupRows);
     uint32_t nib = 0;
     if (c < k) {
         if constexpr (VEC) {
@@ -141,38 +146,52 @@ __global__ __launch_bounds__(256) void outlier_flags_kernel(const float *__restr
                     if (c + e < k && is_outlier(X[(int64_t)r * xsh + c + e], t)) nib |= 1u << e;
         }
     }
-    // eight consecutive lanes hold one 32-column word
-    uint32_t word = nib << (4 * (tid & 7));
-    word |= __shfl_xor(word, 1, 64);
-    word |= __shfl_xor(word, 2, 64);
-    word |= __shfl_xor(word, 4, 64);
-    const int w = blockIdx.x * (kFlagCols / 32) + (tid >> 3);
-    if ((tid & 7) == 0 && w < nwords) {
-        if constexpr (kAcc) {
-            if (word) __hip_atomic_fetch_or(acc + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(partial + (int64_t)blockIdx.y * nwords + w, word, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    if (g > 0) nibs[g - 1][ct] = nib;
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+        for (int j = 0; j < kFlagGroups - 1; ++j) nib |= nibs[j][ct];
+        // eight consecutive lanes hold one 32-column word
+        uint32_t word = nib << (4 * (ct & 7));
+        word |= __shfl_xor(word, 1, 64);
+        word |= __shfl_xor(word, 2, 64);
+        word |= __shfl_xor(word, 4, 64);
+        const int w = blockIdx.x * (kFlagCols / 32) + (ct >> 3);
+        if ((ct & 7) == 0 && w < nwords) {
+            if constexpr (kAcc) {
+                if (word) __hip_atomic_fetch_or(acc + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(partial + (int64_t)blockIdx.y * nwords + w, word, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const unsigned total = gridDim.x * gridDim.y;
     if (tid == 0) {
-        const unsigned a = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = a;
-        // every workgroup has arrived: nobody else touches the ticket in this launch
-        if (a == total - 1) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // blocks b, b + 8, ... share an XCD (round-robin dispatch); the last of each XCD arrives globally
+        const unsigned total = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x, xcd = bid & 7;
+        const unsigned on_xcd = (total - xcd + 7) / 8, xcds = total < 8 ? total : 8;
+        unsigned fin = 0;
+        if (__hip_atomic_fetch_add(ticket + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == on_xcd - 1) {
+            __hip_atomic_store(ticket + xcd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(ticket + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcds - 1) {
+                __hip_atomic_store(ticket + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fin = 1;
+            }
+        }
+        last = fin;
     }
     __syncthreads();
-    if (last != total - 1) return;
+    if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the sc1 loads stay below
-    if constexpr (kAcc) build_index<P>(acc, 1, nwords, bits, rank, idx, wsum, &count);
-    else build_index<P>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count);
+    if constexpr (kAcc) build_index<1, kFlagThreads>(acc, 1, nwords, bits, rank, idx, wsum, &count);
+    else build_index<1, kFlagThreads>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count);
     __syncthreads();  // every accumulator word has been read
     if (tid == 0) idx[0] = count;
     if constexpr (kAcc)
-        for (int i = tid; i < nwords; i += 256) __hip_atomic_store(acc + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = tid; i < nwords; i += kFlagThreads)
+            __hip_atomic_store(acc + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ bool bit_of(const uint32_t *bits, int64_t c) { return (bits[c >> 5] >> (c & 31)) & 1u; }
@@ -258,20 +277,14 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
 template <bool VEC>
 void launch_flags(hipStream_t s, const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v,
                   int slot) {
-    const int nw = v.nwords;
-    const unsigned gx = (unsigned)((k + kFlagCols - 1) / kFlagCols);
-    if (nw <= kAccWords) {
-        // the accumulator path: 16-row chunks (more workgroups in flight; the last one reads nw words, not chunks)
-        int rows = kAccChunkRows;
-        while ((m + rows - 1) / rows > 65535) rows *= 2;
-        const dim3 grid(gx, (unsigned)((m + rows - 1) / rows));
-        outlier_flags_kernel<VEC, 1, true><<<grid, 256, 0, s>>>(X, xsh, m, k, t, rows, v.partial, nw, slot, v.bits, v.rank,
-                                                                v.idx);
-        return;
-    }
-    // K > 32 768: 64-row chunks store their words; the last workgroup ORs every chunk's (one word per thread)
-    outlier_flags_kernel<VEC, 1, false><<<dim3(gx, (unsigned)v.nchunks), 256, 0, s>>>(X, xsh, m, k, t, kChunkRows, v.partial,
-                                                                                      nw, slot, v.bits, v.rank, v.idx);
+    const dim3 grid((unsigned)((k + kFlagCols - 1) / kFlagCols), (unsigned)v.nchunks);
+    // K <= 32 768: the accumulator (the last workgroup reads nwords words); else every chunk's partial words
+    if (v.nwords <= kAccWords)
+        outlier_flags_kernel<VEC, true><<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot, v.bits,
+                                                                      v.rank, v.idx);
+    else
+        outlier_flags_kernel<VEC, false><<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot,
+                                                                       v.bits, v.rank, v.idx);
 }
 
 // column mask, ranks, index list and count of X's outlier columns: ONE launch (the last flags workgroup
