@@ -63,7 +63,8 @@ struct GemmArgs {
     unsigned *tickets;  // tiles words, zeroed before every launch
     const float *bias;  // n floats, added after the dequantize (kEpi >= 1)
     int reset_tickets;  // the reducer re-zeroes its ticket (scratch zeroed once at allocation)
-    // kEpiOutlier: xo [m][cnt], wo [cnt][wo_ld] (16-B aligned rows), cnt = *ocount on the device
+    // kEpiOutlier: the chain's operands where they lie -- xo = X (m x k, row stride xo_ld), wo = W (k x n, row stride
+    // wo_ld) -- at the outlier columns ocols[0 .. cnt) (ascending), cnt = *ocount on the device
     const float *xo;
     const float *wo;
     const int *ocount;
@@ -71,6 +72,8 @@ struct GemmArgs {
     // gemm_i8_fm's full-tile stores: each tile starts its row-pair loop at its own offset (set by the host for
     // output rows of >= 64 KiB, where the tiles' concurrent row writes otherwise meet on the same memory channels)
     int rot_rows;
+    int64_t xo_ld;
+    const int *ocols;
 };
 
 // Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
@@ -220,9 +223,14 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         const_cast<int8_t *>(uniform_ptr(p.B + (((int64_t)tn * 16 + wn * 8) * nsub + u0) * 1024)), 0,
         __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
     const int voff = lane * 16;
-    // kEpiOutlier: the outlier-column count (device-side), read before the k-loop so the epilogue's operand
-    // loads do not wait on it
+    // kEpiOutlier: the outlier-column count (device-side) and the lane's columns of the first two f32-MFMA steps
+    // (t = 4 tt + kq), read before the k-loop so the epilogue's operand loads do not wait on them
     const int ocnt = kEpi == kEpiOutlier ? __builtin_amdgcn_readfirstlane(*p.ocount) : 0;
+    int ocol[2] = {0, 0};
+    if constexpr (kEpi == kEpiOutlier) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) ocol[tt] = 4 * tt + (lane >> 4) < ocnt ? p.ocols[4 * tt + (lane >> 4)] : 0;
+    }
 
     v4i acc[8][8];
 #pragma unroll
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     const int lrow = lane & 15, kq = lane >> 4;
     const int r0 = wm * 128, c0 = wn * 128;
     // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) for both halves, loaded
-    // together here so their latency is paid once: ow[step][ni] = wo[t][col], ox[half][mq][step] = xo[row][t]
+    // together here so their latency is paid once: ow[step][ni] = W[col_t][j], ox[half][mq][step] = X[row][col_t]
     // with t = 4 step + kq; +0 / -0 past the count (see below)
     float ox[2][4][2], ow[2][8];
     if constexpr (kEpi == kEpiOutlier) {
@@ -314,14 +322,16 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         for (int tt = 0; tt < 2; ++tt) {
             const int t = 4 * tt + kq;
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni)
-                ow[tt][ni] = t < ocnt ? p.wo[(int64_t)t * p.wo_ld + gj0 + c0 + ni * 16 + lrow] : -0.0f;
+            for (int ni = 0; ni < 8; ++ni) {
+                const int j = gj0 + c0 + ni * 16 + lrow;
+                ow[tt][ni] = t < ocnt ? (j < p.n ? p.wo[(int64_t)ocol[tt] * p.wo_ld + j] : 0.0f) : -0.0f;
+            }
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
                 for (int mq = 0; mq < 4; ++mq) {
                     const int i = gi0 + r0 + 64 * h + mq * 16 + lrow;
-                    ox[h][mq][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * ocnt + t] : 0.0f;
+                    ox[h][mq][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * p.xo_ld + ocol[tt]] : 0.0f;
                 }
         }
     }
@@ -392,11 +402,14 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
 #pragma unroll 1
                 for (int t0 = 8; t0 < ocnt; t0 += 4) {
                     const int t = t0 + kq;  // the lane's k within the MFMA step
-                    const float xa = t < ocnt && ia < p.m ? p.xo[(int64_t)ia * ocnt + t] : 0.0f;
+                    const int col = t < ocnt ? p.ocols[t] : 0;
+                    const float xa = t < ocnt && ia < p.m ? p.xo[(int64_t)ia * p.xo_ld + col] : 0.0f;
                     float wb[8];
 #pragma unroll
-                    for (int ni = 0; ni < 8; ++ni)
-                        wb[ni] = t < ocnt ? p.wo[(int64_t)t * p.wo_ld + gj0 + c0 + ni * 16 + lrow] : -0.0f;
+                    for (int ni = 0; ni < 8; ++ni) {
+                        const int j = gj0 + c0 + ni * 16 + lrow;
+                        wb[ni] = t < ocnt ? (j < p.n ? p.wo[(int64_t)col * p.wo_ld + j] : 0.0f) : -0.0f;
+                    }
 #pragma unroll
                     for (int ni = 0; ni < 8; ++ni) oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, wb[ni], oc[ni], 0, 0, 0);
                 }

@@ -126,17 +126,16 @@ __device__ __forceinline__ void zero_words_block0(uint32_t *words, int n) {
 // LLM.int8() decomposition inside the pack (outlier.hip builds the mask): feature k of X is an outlier
 // column when bit k of `bits` is set.  The int8 chain runs on X' / W' = X / W with those columns /
 // rows zeroed, so the packs treat them as +0 (absmax candidates, the signed seed and the quantized
-// bytes alike, exactly as packing the zeroed copies), and the pass that holds the original values
-// in registers writes them out compactly for the fp32 part: xo[i * cnt + rank(k)] = X[i,k],
-// wo[rank(k) * wo_ld + j] = W[k,j], rank(k) = outlier columns below k.
+// bytes alike, exactly as packing the zeroed copies).  The fp32 part reads the original values from X and W
+// themselves (gemm_i8_fm<kEpiOutlier>), so nothing is written here.  The flags launch lays the mask out per
+// lane: lanenib[l] nibble j = the bits of X-row chunk l + 64 j (columns 4 (l + 64 j) .. +3), rowbits[q] bit
+// 4 i + e = W row 4 q + e + 1024 i -- one load per lane or thread, no shuffles.
 struct OutlierMask {
-    const uint32_t *bits;  // ceil(K/32) words
-    const int *rank;       // per word: set bits in the words below it
-    const int *count;      // outlier columns (device)
-    float *xo, *wo;
-    int64_t wo_ld;
+    const uint32_t *bits;      // ceil(K/32) words (bit 0 of word 0: column 0, the absmax seed)
+    const int *count;          // outlier columns (device)
+    const uint64_t *lanenib;   // 64 lanes
+    const uint32_t *rowbits;   // 256 W-strip thread rows
 };
-__device__ __forceinline__ bool om_bit(const OutlierMask &om, int k) { return (om.bits[k >> 5] >> (k & 31)) & 1u; }
 
 // ------------------------------------------------------------------------------------------------
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
@@ -175,19 +174,11 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         // buffer loads on one per-lane offset; chunks >= nfull lie past the descriptor and read as zeros
         typedef int v4i_t __attribute__((ext_vector_type(4)));
         const auto rs = buf_rsrc(srow, (uint32_t)nfull * 16);
-        // the mask words (<= 128: two per lane) and their ranks, issued ahead of the row so that they have
-        // arrived with it (no round trip after the row's loads); chunk c needs word (4c) >> 5 = c >> 3
-        uint32_t mw2[2] = {0u, 0u};
-        int mr2[2] = {0, 0};
+        // the lane's mask nibbles (16 chunks), issued ahead of the row so that they arrive with it
+        uint64_t ln = 0;
         if constexpr (kMask) {
-            static_assert(R <= 16, "two mask words per lane cover len <= 4096");
-            const int nw = (len + 31) >> 5;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int wi = min(lane + h * kWave, nw - 1);
-                mw2[h] = om->bits[wi];
-                mr2[h] = om->rank[wi];
-            }
+            static_assert(R <= 16, "the lane table covers len <= 4096");
+            ln = om->lanenib[lane];
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -195,33 +186,16 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
             v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
         if constexpr (kMask) {
-            // outlier columns: their values go to xo, X' holds +0 there (the seed included)
-            const int cnt = *om->count;
-            if (cnt > 0) {
-                if (om_bit(*om, 0)) seed = 0.0f;
-                float *xrow = om->xo + row * cnt;
+            // outlier columns: X' holds +0 there (the seed included); branch-free selects
+            if (*om->count > 0) {
+                if (om->bits[0] & 1u) seed = 0.0f;
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    const int c = lane + j * kWave;
-                    // word (lane >> 3) + 8j lives in lane ((lane >> 3) + 8j) & 63, half j >> 3 (the
-                    // shuffles outside the branches: every lane active)
-                    const int src_lane = ((lane >> 3) + 8 * j) & 63;
-                    const uint32_t mw = (uint32_t)__shfl((int)mw2[j >> 3], src_lane, 64);
-                    const int mr = __shfl(mr2[j >> 3], src_lane, 64);
-                    if (c < nfull) {
-                        const int sh = (4 * c) & 31;
-                        const uint32_t nib = (mw >> sh) & 15u;
-                        if (nib) {
-                            float e4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                if ((nib >> e) & 1u) {
-                                    xrow[mr + __popc(mw & ((1u << (sh + e)) - 1u))] = e4[e];
-                                    e4[e] = 0.0f;
-                                }
-                            v[j] = make_float4(e4[0], e4[1], e4[2], e4[3]);
-                        }
-                    }
+                    const uint32_t nib = (uint32_t)(ln >> (4 * j)) & 15u;
+                    v[j].x = (nib & 1u) ? 0.0f : v[j].x;
+                    v[j].y = (nib & 2u) ? 0.0f : v[j].y;
+                    v[j].z = (nib & 4u) ? 0.0f : v[j].z;
+                    v[j].w = (nib & 8u) ? 0.0f : v[j].w;
                 }
             }
         }
@@ -1000,19 +974,9 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     const float w_seed = t < kWs8Cols ? w[n0 + t] : 0.0f;  // W[0, j], issued first (used after the reduction)
     const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kWs8Cols) * 4));
     const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c2) * 4);
-    // mask words of this thread's rows (word (4 rq + 1024 i) >> 5 for every e) and their ranks, issued
-    // ahead of the strip's loads
-    uint32_t mw[4];
-    int mr[4];
-    if constexpr (kMask) {
-        const int nw = (k + 31) >> 5;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int wi = min((4 * rq + 1024 * i) >> 5, nw - 1);
-            mw[i] = om->bits[wi];
-            mr[i] = om->rank[wi];
-        }
-    }
+    // the thread's mask bits (its 16 rows), issued ahead of the strip's loads
+    uint32_t rb = 0;
+    if constexpr (kMask) rb = om->rowbits[rq];
     float4 v[4][4];  // [i][e]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1023,19 +987,18 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
         }
     bool seed_masked = false;
     if constexpr (kMask) {
-        // outlier rows of W (outlier feature columns of X): their values go to wo, W' holds +0 there
+        // outlier rows of W (outlier feature columns of X): W' holds +0 there; branch-free selects
         if (*om->count > 0) {
-            seed_masked = om_bit(*om, 0);
+            seed_masked = om->bits[0] & 1u;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int r = 4 * rq + e + 1024 * i, b = r & 31;
-                    if (r < k && ((mw[i] >> b) & 1u)) {
-                        const int rk = mr[i] + __popc(mw[i] & ((1u << b) - 1u));
-                        *reinterpret_cast<float4 *>(om->wo + rk * om->wo_ld + n0 + 4 * c2) = v[i][e];
-                        v[i][e] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
+                    const bool z = (rb >> (4 * i + e)) & 1u;
+                    v[i][e].x = z ? 0.0f : v[i][e].x;
+                    v[i][e].y = z ? 0.0f : v[i][e].y;
+                    v[i][e].z = z ? 0.0f : v[i][e].z;
+                    v[i][e].w = z ? 0.0f : v[i][e].w;
                 }
         }
     }
@@ -1310,14 +1273,13 @@ bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, cons
 
 hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
                                            int64_t wsh, int n, PackedView outw, float range, const uint32_t *bits,
-                                           const int *rank, const int *count, float *xo, float *wo, int64_t wo_ld,
+                                           const int *count, const uint64_t *lanenib, const uint32_t *rowbits,
                                            hipStream_t stream) {
-    if (!pack_single_pass_outlier_ok(x, xsh, m, k, w, wsh, n) || (reinterpret_cast<uintptr_t>(wo) & 15) || (wo_ld & 3))
-        return hipErrorNotSupported;
+    if (!pack_single_pass_outlier_ok(x, xsh, m, k, w, wsh, n)) return hipErrorNotSupported;
     const int nstrips = n / kWs8Cols;
     const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
     const int nx = (int)(outx.rows_pad / 8);
-    const OutlierMask om{bits, rank, count, xo, wo, wo_ld};
+    const OutlierMask om{bits, count, lanenib, rowbits};
     // a 4-waves-per-SIMD register budget (102 VGPRs, the same two blocks per CU): at 5 the masked body spilled
     // 20 B per lane (profiles/r03_ab_maskpack_wpe.log)
     pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(
