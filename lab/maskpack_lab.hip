@@ -67,7 +67,7 @@ int main(int argc, char **argv) {
         else if (mode == 1) CK(outlier_scan(X, k, m, k, t, v2, s0));
         else sweep_kernel<<<1024, 256, 0, s0>>>(X, (int64_t)m * k / 4, v2.partial);
     };
-    const OutlierMask om{v.bits, v.idx, v.lanenib, v.rowbits};
+    const OutlierMask om{v.bits, v.idx, v.lanenib, v.lanerank, v.rowbits, v.xm};
     auto pack = [&](int var) {
         if (var == 0)
             pack_single_pass8_kernel<5><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n, n,
