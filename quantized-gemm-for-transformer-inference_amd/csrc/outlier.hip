@@ -31,7 +31,8 @@ namespace qgemm {
 // The flags launch's arrival tickets: a zero-initialised array of the code object (per device), one 128-B line per
 // slot, one slot per stream (outlier_ticket_slot).  Each launch's last workgroup re-zeroes its slot, so a slot is 0
 // between calls -- without any allocation or memset, so the first call on a stream may be inside a graph capture.
-constexpr int kTicketSlots = 256, kTicketStride = 32;
+// a slot = 9 counters (8 per-XCD + 1 global), each on a 128-B line of its own
+constexpr int kTicketSlots = 256, kCounterWords = 32, kTicketStride = 9 * kCounterWords;
 __device__ unsigned g_flags_ticket[kTicketSlots * kTicketStride];
 // K <= 32 768 (kAccWords words of 32 columns): each flags workgroup ORs its nonzero mask words into the slot's
 // accumulator with agent-scope atomics (performed at the memory side, coherent across XCDs), so the last workgroup
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
                                                                      uint64_t *__restrict__ lanenib,
                                                                      uint16_t *__restrict__ lanerank,
                                                                      uint32_t *__restrict__ rowbits) {
-    unsigned *ticket = g_flags_ticket + slot * kTicketStride;  // [0..7]: per-XCD counters, [16]: the global one
+    unsigned *ticket = g_flags_ticket + slot * kTicketStride;  // counter x (x < 8: per XCD, 8: global) at x * 32
     uint32_t *acc = g_flags_acc + slot * kAccWords;
     __shared__ int wsum[kFlagThreads / 64];
     __shared__ uint32_t nibs[kFlagGroups - 1][256];
@@ -182,10 +183,11 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
         const unsigned total = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x, xcd = bid & 7;
         const unsigned on_xcd = (total - xcd + 7) / 8, xcds = total < 8 ? total : 8;
         unsigned fin = 0;
-        if (__hip_atomic_fetch_add(ticket + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == on_xcd - 1) {
-            __hip_atomic_store(ticket + xcd, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__hip_atomic_fetch_add(ticket + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcds - 1) {
-                __hip_atomic_store(ticket + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned *mine = ticket + xcd * kCounterWords, *all = ticket + 8 * kCounterWords;
+        if (__hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == on_xcd - 1) {
+            __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(all, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcds - 1) {
+                __hip_atomic_store(all, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 fin = 1;
             }
         }
