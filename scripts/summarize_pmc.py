@@ -20,7 +20,7 @@ from collections import defaultdict
 def short(name):
     if "mm_f32" in name and "<" in name:  # keep the tile configuration: attention QK^T and PV differ
         return "mm_f32<" + name.split("<")[1].split(">")[0] + ">"
-    for key in ("gemm_i8", "pack_single_pass", "pack_rows_and_colmax", "pack_cols", "pack_rows", "colmax",
+    for key in ("gemm_i8", "outlier_flags", "pack_single_pass", "pack_rows_and_colmax", "pack_cols", "pack_rows", "colmax",
                 "fill_uniform", "mm_f32", "error_partials", "error_final", "error_reference_mean"):
         if key in name:
             return key
