@@ -202,31 +202,32 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
     __syncthreads();  // every accumulator word has been read; sbits is complete
     if (tid == 0) idx[0] = count;
     if (nwords <= kLaneWords) {
-        // the masked pack's tables (K <= 4096): lanenib[l] nibble j = the mask nibble of X-row chunk c = l + 64 j
-        // (columns 4c .. 4c + 3: word c >> 3, shift 4 (c & 7)); lanerank[l][j] = the outlier columns below 4c (the
-        // chunk's first xo slot); rowbits[q] bit 4 i + e = W row 4 q + e + 1024 i
-        if (tid < 64) {
-            uint64_t v = 0;
+        // the masked pack's tables (K <= 4096), one entry per thread: lanenib[l] nibble j = the mask nibble of X-row
+        // chunk c = l + 64 j (columns 4c .. 4c + 3: word c >> 3, shift 4 (c & 7)); lanerank[l][j] = the outlier
+        // columns below 4c (the chunk's first xo slot); rowbits[q] bit 4 i + e = W row 4 q + e + 1024 i
+        __shared__ uint32_t snib[64][2], srow[256];
+        if (tid < 128) snib[tid >> 1][tid & 1] = 0u;
+        if (tid < 256) srow[tid] = 0u;
+        __syncthreads();
+        {
+            const int l = tid & 63, j = tid >> 6;  // 1024 threads = 64 lanes x 16 chunks
+            const int c = l + 64 * j, w = c >> 3, sh = 4 * (c & 7);
+            const uint32_t wd = w < nwords ? sbits[w] : 0u;
+            const uint32_t nb = (wd >> sh) & 15u;
+            lanerank[l * 16 + j] = (uint16_t)(w < nwords ? srank[w] + __popc(wd & ((1u << sh) - 1u)) : 0);
+            if (nb) atomicOr(&snib[l][j >> 3], nb << (4 * (j & 7)));
+            const int q = tid & 255, i = tid >> 8;  // 256 W-strip threads x 4 row blocks
+            uint32_t rb = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int c = tid + 64 * j, w = c >> 3, sh = 4 * (c & 7);
-                const uint32_t wd = w < nwords ? sbits[w] : 0u;
-                v |= (uint64_t)((wd >> sh) & 15u) << (4 * j);
-                lanerank[tid * 16 + j] = (uint16_t)(w < nwords ? srank[w] + __popc(wd & ((1u << sh) - 1u)) : 0);
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * q + e + 1024 * i;
+                if (r < k && ((sbits[r >> 5] >> (r & 31)) & 1u)) rb |= 1u << (4 * i + e);
             }
-            lanenib[tid] = v;
-        } else if (tid >= 256 && tid < 512) {
-            const int q = tid - 256;
-            uint32_t v = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int r = 4 * q + e + 1024 * i;
-                    if (r < k && ((sbits[r >> 5] >> (r & 31)) & 1u)) v |= 1u << (4 * i + e);
-                }
-            rowbits[q] = v;
+            if (rb) atomicOr(&srow[q], rb);
         }
+        __syncthreads();
+        if (tid < 64) lanenib[tid] = (uint64_t)snib[tid][0] | ((uint64_t)snib[tid][1] << 32);
+        if (tid < 256) rowbits[tid] = srow[tid];
     }
     if constexpr (kAcc)
         for (int i = tid; i < nwords; i += kFlagThreads)
