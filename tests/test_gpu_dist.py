@@ -135,3 +135,20 @@ def test_one_rccl_with_torch_process_group(qg, device):
         assert "torch" in rccl[0], rccl
     finally:
         dist.destroy_process_group()
+
+
+def test_bench_line_names_its_world_and_binary(qg):
+    """One short bench.py run on the GPU (the driver's contract at N = 1): the line reports n_gpus 1 and the
+    world RCCL itself sees for the product communicator, the library's source hash equal to this tree's, and the
+    whole-node C4 figure with the serial and the pipelined gather both leaving the shards' rows bit-identical."""
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-error-stats", "--cold-steps", "0", "--node-reps", "1",
+                        "--prewarm-ms", "0"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["n_gpus"] == 1 and js["rccl_world"] == 1
+    assert f"src={qg.source_hash()}" in js["library"]
+    node = js["c4_node"]
+    assert node["gathered_rows_match_one_gpu"] is True and node["pipelined"]["gathered_rows_match_one_gpu"] is True
