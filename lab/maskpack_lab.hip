@@ -31,6 +31,37 @@ __global__ void sweep_kernel(const float *X, int64_t n4, uint32_t *sink) {
     if (a == 12345.f) sink[0] = 1u;  // keeps the loads
 }
 
+// the product flags launch's streaming part alone (same grid, loads, LDS combine, atomics into a scratch word array;
+// no arrival counters, no last-workgroup index build): flags - flags_notail = the tail
+__global__ __launch_bounds__(1024) void flags_notail_kernel(const float *__restrict__ X, int64_t xsh, int m, int k,
+                                                            float t, uint32_t *__restrict__ acc, int nwords) {
+    __shared__ uint32_t nibs[3][256];
+    const int tid = threadIdx.x, ct = tid & 255, g = tid >> 8;
+    const int c = blockIdx.x * 1024 + 4 * ct;
+    const int r0 = blockIdx.y * 64 + g * 16, r1 = min(m, r0 + 16);
+    uint32_t nib = 0;
+    if (c < k) {
+        const float *p = X + (int64_t)r0 * xsh + c;
+#pragma unroll 16
+        for (int r = r0; r < r1; ++r, p += xsh) {
+            const float4 x = *reinterpret_cast<const float4 *>(p);
+            nib |= (is_outlier(x.x, t) ? 1u : 0u) | (is_outlier(x.y, t) ? 2u : 0u) | (is_outlier(x.z, t) ? 4u : 0u) |
+                   (is_outlier(x.w, t) ? 8u : 0u);
+        }
+    }
+    if (g > 0) nibs[g - 1][ct] = nib;
+    __syncthreads();
+    if (g == 0) {
+        for (int j = 0; j < 3; ++j) nib |= nibs[j][ct];
+        uint32_t word = nib << (4 * (ct & 7));
+        word |= __shfl_xor(word, 1, 64);
+        word |= __shfl_xor(word, 2, 64);
+        word |= __shfl_xor(word, 4, 64);
+        const int w = blockIdx.x * 32 + (ct >> 3);
+        if ((ct & 7) == 0 && w < nwords && word) __hip_atomic_fetch_or(acc + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __global__ void put_outliers(float *X, int m, int k, int every, int ncols) {
     // ncols columns spread over k (bench.py outlier_columns), every `every`-th row |x| = 30
     const int c = blockIdx.x, i = threadIdx.x + blockIdx.y * 256;
@@ -61,11 +92,13 @@ int main(int argc, char **argv) {
     const float range = 127.f;
     const OutlierScratch v2 = scratch_view(scr2, m, k);
     // mode 0: flags into the pack's scratch; 1: flags into scratch2 (the pack's mask words were written long ago);
-    // 2: a plain read sweep of X instead of flags
+    // 2: a plain read sweep of X instead of flags; 3: the flags launch's streaming part alone (flags_notail_kernel)
     auto flags = [&](float t, int mode = 0) {
         if (mode == 0) CK(outlier_scan(X, k, m, k, t, v, s0));
         else if (mode == 1) CK(outlier_scan(X, k, m, k, t, v2, s0));
-        else sweep_kernel<<<1024, 256, 0, s0>>>(X, (int64_t)m * k / 4, v2.partial);
+        else if (mode == 2) sweep_kernel<<<1024, 256, 0, s0>>>(X, (int64_t)m * k / 4, v2.partial);
+        else flags_notail_kernel<<<dim3((k + 1023) / 1024, (m + 63) / 64), 1024, 0, s0>>>(X, k, m, k, t, v2.partial,
+                                                                                         (k + 31) / 32);
     };
     const OutlierMask om{v.bits, v.idx, v.lanenib, v.lanerank, v.rowbits, v.xm};
     auto pack = [&](int var) {
@@ -84,7 +117,8 @@ int main(int argc, char **argv) {
     struct V { std::string name; int pack; float t; bool with_flags; int fmode; };
     std::vector<V> vs = {{"plain", 0, 6.f, true, 0}, {"mask", 1, 6.f, true, 0}, {"mask5", 2, 6.f, true, 0},
                          {"mask0", 1, 1e30f, true, 0}, {"plain_alone", 0, 6.f, false, 0}, {"mask_alone", 1, 6.f, false, 0},
-                         {"mask_flags2", 1, 6.f, true, 1}, {"mask_sweep", 1, 6.f, true, 2}, {"plain_sweep", 0, 6.f, true, 2}};
+                         {"mask_flags2", 1, 6.f, true, 1}, {"mask_sweep", 1, 6.f, true, 2}, {"plain_sweep", 0, 6.f, true, 2},
+                         {"mask_notail", 1, 6.f, true, 3}};
     // bit check: mask vs mask5
     std::vector<int8_t> a(vx.rows_pad * vx.k_pad), b(a.size());
     flags(6.f); pack(1); CK(hipStreamSynchronize(s0));
