@@ -100,7 +100,7 @@ int main(int argc, char **argv) {
         else flags_notail_kernel<<<dim3((k + 1023) / 1024, (m + 63) / 64), 1024, 0, s0>>>(X, k, m, k, t, v2.partial,
                                                                                          (k + 31) / 32);
     };
-    const OutlierMask om{v.bits, v.idx, v.lanenib, v.lanerank, v.rowbits, v.xm};
+    const OutlierMask om{v.bits, v.idx, v.lanenib, v.rowbits};
     auto pack = [&](int var) {
         if (var == 0)
             pack_single_pass8_kernel<5><<<g, 512, 0, s0>>>(X, k, m, k, vx.scale, vx.q, vx.rows_pad, vx.k_pad, W, n, n,

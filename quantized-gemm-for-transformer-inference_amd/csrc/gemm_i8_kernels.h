@@ -63,8 +63,8 @@ struct GemmArgs {
     unsigned *tickets;  // tiles words, zeroed before every launch
     const float *bias;  // n floats, added after the dequantize (kEpi >= 1)
     int reset_tickets;  // the reducer re-zeroes its ticket (scratch zeroed once at allocation)
-    // kEpiOutlier: the chain's operands -- xo [m][cnt] (X's outlier values, compact), wo = W (k x n, row stride wo_ld)
-    // at its rows ocols[0 .. cnt) (the outlier columns, ascending), cnt = *ocount on the device
+    // kEpiOutlier: the chain's operands where they lie -- xo = X (m x k, row stride xo_ld), wo = W (k x n, row stride
+    // wo_ld) -- at the outlier columns ocols[0 .. cnt) (ascending), cnt = *ocount on the device
     const float *xo;
     const float *wo;
     const int *ocount;
@@ -72,6 +72,7 @@ struct GemmArgs {
     // gemm_i8_fm's full-tile stores: each tile starts its row-pair loop at its own offset (set by the host for
     // output rows of >= 64 KiB, where the tiles' concurrent row writes otherwise meet on the same memory channels)
     int rot_rows;
+    int64_t xo_ld;
     const int *ocols;
 };
 
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     const int lrow = lane & 15, kq = lane >> 4;
     const int r0 = wm * 128, c0 = wn * 128;
     // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) for both halves, loaded
-    // together here so their latency is paid once: ow[step][ni] = W[col_t][j], ox[half][mq][step] = xo[row][t]
+    // together here so their latency is paid once: ow[step][ni] = W[col_t][j], ox[half][mq][step] = X[row][col_t]
     // with t = 4 step + kq; +0 / -0 past the count (see below)
     float ox[2][4][2], ow[2][8];
     if constexpr (kEpi == kEpiOutlier) {
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
 #pragma unroll
                 for (int mq = 0; mq < 4; ++mq) {
                     const int i = gi0 + r0 + 64 * h + mq * 16 + lrow;
-                    ox[h][mq][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * ocnt + t] : 0.0f;
+                    ox[h][mq][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * p.xo_ld + ocol[tt]] : 0.0f;
                 }
         }
     }
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
                 for (int t0 = 8; t0 < ocnt; t0 += 4) {
                     const int t = t0 + kq;  // the lane's k within the MFMA step
                     const int col = t < ocnt ? p.ocols[t] : 0;
-                    const float xa = t < ocnt && ia < p.m ? p.xo[(int64_t)ia * ocnt + t] : 0.0f;
+                    const float xa = t < ocnt && ia < p.m ? p.xo[(int64_t)ia * p.xo_ld + col] : 0.0f;
                     float wb[8];
 #pragma unroll
                     for (int ni = 0; ni < 8; ++ni) {

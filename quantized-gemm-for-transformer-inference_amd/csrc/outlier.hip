@@ -14,10 +14,9 @@
 //                    last ORs the chunk masks into the column mask, the per-word ranks, the ascending list
 //                    of outlier columns and their count (stays on the device; round 5: no index launch)
 //   the pack       : the single pass with the mask (pack.hip): X'/W' quantized without materialising
-//                    them (per-lane nibble / slot / row-bit tables the flags launch builds: no shuffles); each X
-//                    row's outlier values gathered in LDS and written as one contiguous xo row ([m][cnt])
-//   the GEMM       : the int8 part with the fp32 chain added in its store epilogue (gemm_i8_kernels.h): X's
-//                    outlier values from xo, W's outlier rows where they lie
+//                    them (per-lane nibble / row-bit tables the flags launch builds: no shuffles, no stores)
+//   the GEMM       : the int8 part with the fp32 chain added in its store epilogue (gemm_i8_kernels.h), its
+//                    operands read from X's outlier columns and W's outlier rows where they lie
 // Other shapes: flags + index, X'/W' materialised by a masking pass, the plain drop-in on them, and a
 // correction kernel adding the chain to O.
 #include <algorithm>
@@ -58,7 +57,7 @@ __device__ __forceinline__ bool is_outlier(float a, float b) {
 template <int P, int kThreads>
 __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial, int nchunks, int nwords,
                                             uint32_t *__restrict__ bits, int *__restrict__ rank, int *__restrict__ idx,
-                                            int *wsum, int *base, uint32_t *sbits, int *srank /* LDS, words < kLaneWords */) {
+                                            int *wsum, int *base, uint32_t *sbits /* LDS, words < kLaneWords */) {
     constexpr int kWaves = kThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s = tid % P;
@@ -98,7 +97,7 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
         if (s == 0 && w < nwords) {
             bits[w] = word;
             rank[w] = below;
-            if (w < kLaneWords) sbits[w] = word, srank[w] = below;
+            if (w < kLaneWords) sbits[w] = word;
             int j = 0;
             for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
         }
@@ -126,14 +125,12 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
                                                                      int nwords, int slot, uint32_t *__restrict__ bits,
                                                                      int *__restrict__ rank, int *__restrict__ idx,
                                                                      uint64_t *__restrict__ lanenib,
-                                                                     uint16_t *__restrict__ lanerank,
                                                                      uint32_t *__restrict__ rowbits) {
     unsigned *ticket = g_flags_ticket + slot * kTicketStride;  // counter x (x < 8: per XCD, 8: global) at x * 32
     uint32_t *acc = g_flags_acc + slot * kAccWords;
     __shared__ int wsum[kFlagThreads / 64];
     __shared__ uint32_t nibs[kFlagGroups - 1][256];
     __shared__ uint32_t sbits[kLaneWords];
-    __shared__ int srank[kLaneWords];
     __shared__ unsigned last;
     __shared__ int count;
     const int tid = threadIdx.x, ct = tid & 255, g = tid >> 8;
@@ -196,15 +193,14 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
     __syncthreads();
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the sc1 loads stay below
-    if constexpr (kAcc) build_index<1, kFlagThreads>(acc, 1, nwords, bits, rank, idx, wsum, &count, sbits, srank);
-    else build_index<1, kFlagThreads>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count, sbits,
-                                      srank);
+    if constexpr (kAcc) build_index<1, kFlagThreads>(acc, 1, nwords, bits, rank, idx, wsum, &count, sbits);
+    else build_index<1, kFlagThreads>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count, sbits);
     __syncthreads();  // every accumulator word has been read; sbits is complete
     if (tid == 0) idx[0] = count;
     if (nwords <= kLaneWords) {
         // the masked pack's tables (K <= 4096), one entry per thread: lanenib[l] nibble j = the mask nibble of X-row
-        // chunk c = l + 64 j (columns 4c .. 4c + 3: word c >> 3, shift 4 (c & 7)); lanerank[l][j] = the outlier
-        // columns below 4c (the chunk's first xo slot); rowbits[q] bit 4 i + e = W row 4 q + e + 1024 i
+        // chunk c = l + 64 j (columns 4c .. 4c + 3: word c >> 3, shift 4 (c & 7)); rowbits[q] bit 4 i + e = W row
+        // 4 q + e + 1024 i
         __shared__ uint32_t snib[64][2], srow[256];
         if (tid < 128) snib[tid >> 1][tid & 1] = 0u;
         if (tid < 256) srow[tid] = 0u;
@@ -214,7 +210,6 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
             const int c = l + 64 * j, w = c >> 3, sh = 4 * (c & 7);
             const uint32_t wd = w < nwords ? sbits[w] : 0u;
             const uint32_t nb = (wd >> sh) & 15u;
-            lanerank[l * 16 + j] = (uint16_t)(w < nwords ? srank[w] + __popc(wd & ((1u << sh) - 1u)) : 0);
             if (nb) atomicOr(&snib[l][j >> 3], nb << (4 * (j & 7)));
             const int q = tid & 255, i = tid >> 8;  // 256 W-strip threads x 4 row blocks
             uint32_t rb = 0;
@@ -288,7 +283,6 @@ struct OutlierScratch {
     uint32_t *partial, *bits;
     int *rank, *idx;    // idx[0] = count, idx[1 ..] = the outlier columns ascending
     uint64_t *lanenib;  // fast path: per-lane X-row chunk nibbles (64)
-    uint16_t *lanerank; // fast path: per-lane, per-chunk first xo slot (64 x 16)
     uint32_t *rowbits;  // fast path: per-thread W-strip row bits (256)
     float *xm, *wm;     // X' / W' (fallback)
     int nchunks, nwords;
@@ -311,8 +305,6 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
     p += a256(sizeof(int) * v.nwords);
     v.lanenib = reinterpret_cast<uint64_t *>(p);
     p += a256(sizeof(uint64_t) * 64);
-    v.lanerank = reinterpret_cast<uint16_t *>(p);
-    p += a256(sizeof(uint16_t) * 64 * 16);
     v.rowbits = reinterpret_cast<uint32_t *>(p);
     p += a256(sizeof(uint32_t) * 256);
     v.partial = reinterpret_cast<uint32_t *>(p);
@@ -330,11 +322,10 @@ void launch_flags(hipStream_t s, const float *X, int64_t xsh, int m, int k, floa
     // K <= 32 768: the accumulator (the last workgroup reads nwords words); else every chunk's partial words
     if (v.nwords <= kAccWords)
         outlier_flags_kernel<VEC, true><<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot, v.bits,
-                                                                      v.rank, v.idx, v.lanenib, v.lanerank, v.rowbits);
+                                                                      v.rank, v.idx, v.lanenib, v.rowbits);
     else
         outlier_flags_kernel<VEC, false><<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot,
-                                                                       v.bits, v.rank, v.idx, v.lanenib, v.lanerank,
-                                                                       v.rowbits);
+                                                                       v.bits, v.rank, v.idx, v.lanenib, v.rowbits);
 }
 
 // column mask, ranks, index list and count of X's outlier columns: ONE launch (the last flags workgroup
@@ -354,7 +345,7 @@ hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, cons
 size_t outlier_scratch_bytes(int m, int n, int k) {
     const size_t nchunks = (size_t)(m + kChunkRows - 1) / kChunkRows, nwords = (size_t)(k + 31) / 32;
     return a256(sizeof(uint32_t) * nchunks * nwords) + a256(sizeof(uint32_t) * nwords) + a256(sizeof(int) * nwords) +
-           a256(sizeof(uint64_t) * 64) + a256(sizeof(uint16_t) * 64 * 16) + a256(sizeof(uint32_t) * 256) +
+           a256(sizeof(uint64_t) * 64) + a256(sizeof(uint32_t) * 256) +
            a256(sizeof(int) * ((size_t)k + 1)) + a256(sizeof(float) * (size_t)m * k) +
            a256(sizeof(float) * (size_t)k * (size_t)round_up(n, 256));
 }
@@ -370,13 +361,13 @@ hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, 
     const OutlierScratch v = scratch_view(scratch, m, k);
     hipError_t e = outlier_scan(X, k, m, k, t, v, s);
     if (e != hipSuccess) return e;
-    e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, v.bits, v.idx, v.lanenib, v.lanerank,
-                                        v.rowbits, v.xm, s);
+    e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, v.bits, v.idx, v.lanenib, v.rowbits, s);
     if (e == hipErrorNotSupported) return hipErrorUnknown;  // scan already enqueued: the envelope checks above disagree
     if (e != hipSuccess) return e;
     const float inv_r2 = 1.0f / (range * range);
-    // the fp32 chain: X's outlier values compacted by the pack (xo [m][cnt]), W's outlier rows where they lie
-    return launch_gemm_dequant_outlier(va, vb, O, n, m, n, inv_r2, v.xm, W, n, v.idx + 1, v.idx, s);
+    // the fp32 chain reads the outlier columns of X and rows of W where they lie (the column list idx + 1); a compact
+    // copy of X's outlier values written by the pack measured slower (profiles/r05_maskpack_lab_xo_staged.log)
+    return launch_gemm_dequant_outlier(va, vb, O, n, m, n, inv_r2, X, k, W, n, v.idx + 1, v.idx, s);
 }
 
 // Fallback phase 1: flags, indices, X', W' into scratch; the caller then runs the int8 chain on (X', W')

@@ -126,18 +126,15 @@ __device__ __forceinline__ void zero_words_block0(uint32_t *words, int n) {
 // LLM.int8() decomposition inside the pack (outlier.hip builds the mask): feature k of X is an outlier
 // column when bit k of `bits` is set.  The int8 chain runs on X' / W' = X / W with those columns /
 // rows zeroed, so the packs treat them as +0 (absmax candidates, the signed seed and the quantized
-// bytes alike, exactly as packing the zeroed copies).  The X rows' original outlier values go out compactly
-// for the fp32 part, xo[i * cnt + rank(k)] = X[i,k] (gathered in LDS, one contiguous store per row); W's outlier
-// rows the GEMM reads in place.  The flags launch lays the mask out per lane: lanenib[l] nibble j = the bits of
-// X-row chunk l + 64 j (columns 4 (l + 64 j) .. +3), lanerank[l][j] = that chunk's first xo slot, rowbits[q]
-// bit 4 i + e = W row 4 q + e + 1024 i -- loads per lane or thread issued with the data, no shuffles.
+// bytes alike, exactly as packing the zeroed copies).  The fp32 part reads the original values from X and W
+// themselves (gemm_i8_fm<kEpiOutlier>), so nothing is written here.  The flags launch lays the mask out per
+// lane: lanenib[l] nibble j = the bits of X-row chunk l + 64 j (columns 4 (l + 64 j) .. +3), rowbits[q] bit
+// 4 i + e = W row 4 q + e + 1024 i -- one load per lane or thread, no shuffles.
 struct OutlierMask {
     const uint32_t *bits;      // ceil(K/32) words (bit 0 of word 0: column 0, the absmax seed)
     const int *count;          // outlier columns (device)
     const uint64_t *lanenib;   // 64 lanes
-    const uint16_t *lanerank;  // 64 lanes x 16 chunks
     const uint32_t *rowbits;   // 256 W-strip thread rows
-    float *xo;                 // [m][cnt]
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -150,8 +147,7 @@ template <int R, bool kMask = false, bool kWT = false, bool kStage = false>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
-                                                   const OutlierMask *om = nullptr, uint32_t *stage = nullptr,
-                                                   float *ostage = nullptr /* kMask: 64 floats of this wave's LDS */) {
+                                                   const OutlierMask *om = nullptr, uint32_t *stage = nullptr) {
     static_assert(!kMask || R > 0, "the outlier mask needs the register-resident rows");
     const int lane = threadIdx.x & 63;
     const int64_t row = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
@@ -178,14 +174,11 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         // buffer loads on one per-lane offset; chunks >= nfull lie past the descriptor and read as zeros
         typedef int v4i_t __attribute__((ext_vector_type(4)));
         const auto rs = buf_rsrc(srow, (uint32_t)nfull * 16);
-        // the lane's mask nibbles and xo slots (16 chunks), issued ahead of the row so that they arrive with it
+        // the lane's mask nibbles (16 chunks), issued ahead of the row so that they arrive with it
         uint64_t ln = 0;
-        uint4 lr[2] = {};
         if constexpr (kMask) {
             static_assert(R <= 16, "the lane table covers len <= 4096");
             ln = om->lanenib[lane];
-            lr[0] = reinterpret_cast<const uint4 *>(om->lanerank + 16 * lane)[0];
-            lr[1] = reinterpret_cast<const uint4 *>(om->lanerank + 16 * lane)[1];
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -193,35 +186,9 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
             v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
         if constexpr (kMask) {
-            // outlier columns: their values go to xo (gathered in this wave's 64-float LDS stage), X' holds +0 there
-            // (the seed included); branch-free selects
-            const int cnt = *om->count;
-            if (cnt > 0) {
+            // outlier columns: X' holds +0 there (the seed included); branch-free selects
+            if (*om->count > 0) {
                 if (om->bits[0] & 1u) seed = 0.0f;
-                if (__ballot(ln != 0)) {
-                    // cnt <= 64: gathered in LDS, then ONE contiguous store of the row's cnt values; more columns:
-                    // each value stored to its slot directly
-                    const bool staged = cnt <= kWave;
-                    float *xrow = om->xo + row * cnt;
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        const uint32_t nib = (uint32_t)(ln >> (4 * j)) & 15u;
-                        if (nib) {
-                            const uint32_t wv = j < 8 ? (&lr[0].x)[j >> 1] : (&lr[1].x)[(j - 8) >> 1];
-                            const int base = (int)((wv >> (16 * (j & 1))) & 0xffffu);
-                            const float e4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                if ((nib >> e) & 1u) {
-                                    const int slot = base + __popc(nib & ((1u << e) - 1u));
-                                    if (staged) ostage[slot] = e4[e];
-                                    else xrow[slot] = e4[e];
-                                }
-                        }
-                    }
-                    // one wave: its LDS writes precede its reads
-                    if (staged && lane < cnt) xrow[lane] = ostage[lane];
-                }
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     const uint32_t nib = (uint32_t)(ln >> (4 * j)) & 15u;
@@ -1122,7 +1089,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
     OutlierMask om = OutlierMask{}) {
     __shared__ float red[8 * 8 + 8];
     __shared__ __attribute__((aligned(16))) uint32_t xstage[8 * kStageRowWordsMax];  // X rows, LDS-staged
-    __shared__ float ostage[kMask ? 8 * 64 : 1];  // kMask: per wave, one row's outlier values in xo order
     zero_words_block0(zero_words, nzero);
     const int npad = (int)((w_rows_pad - n) / kWs8Cols);
     const int bid = blockIdx.x;
@@ -1141,7 +1107,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         const int64_t xb = bid - nstrips - npad;
         const int rsw = (int)(k_pad >> 2) + 16;
         pack_rows_vec_body<16, kMask, false, true>(xb * 2, x, xsh, m, k, range, x_scale, x_q, x_rows_pad, k_pad, &om,
-                                                   xstage + (threadIdx.x >> 6) * rsw, ostage + (kMask ? (threadIdx.x >> 6) * 64 : 0));
+                                                   xstage + (threadIdx.x >> 6) * rsw);
         __syncthreads();
         write_staged_rows<8>(xstage, rsw, x_q, xb * 8, k_pad);
     }
@@ -1307,13 +1273,13 @@ bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, cons
 
 hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
                                            int64_t wsh, int n, PackedView outw, float range, const uint32_t *bits,
-                                           const int *count, const uint64_t *lanenib, const uint16_t *lanerank,
-                                           const uint32_t *rowbits, float *xo, hipStream_t stream) {
+                                           const int *count, const uint64_t *lanenib, const uint32_t *rowbits,
+                                           hipStream_t stream) {
     if (!pack_single_pass_outlier_ok(x, xsh, m, k, w, wsh, n)) return hipErrorNotSupported;
     const int nstrips = n / kWs8Cols;
     const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
     const int nx = (int)(outx.rows_pad / 8);
-    const OutlierMask om{bits, count, lanenib, lanerank, rowbits, xo};
+    const OutlierMask om{bits, count, lanenib, rowbits};
     // a 4-waves-per-SIMD register budget (102 VGPRs, the same two blocks per CU): at 5 the masked body spilled
     // 20 B per lane (profiles/r03_ab_maskpack_wpe.log)
     pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(

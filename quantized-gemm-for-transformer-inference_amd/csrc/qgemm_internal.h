@@ -142,14 +142,13 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
                                         uint32_t *zero_words = nullptr, int nzero = 0);
 // The single-pass pack (8-column W strips) of the LLM.int8() decomposition's int8 part: outlier columns
 // of X / rows of W packed as +0 (lanenib: per lane l, nibble j = the outlier bits of X-row chunk l + 64 j;
-// lanerank[l][j]: that chunk's first slot in the row's compact outlier values xo [m][cnt]; rowbits: per W-strip
-// thread q, bit 4 i + e = W row 4 q + e + 1024 i; bits[0] bit 0 = column 0, the seed; outlier.hip builds them).
-// hipErrorNotSupported outside the single pass's envelope (K % 4 == 0 too).
+// rowbits: per W-strip thread q, bit 4 i + e = W row 4 q + e + 1024 i; bits[0] bit 0 = column 0, the seed;
+// outlier.hip builds them).  hipErrorNotSupported outside the single pass's envelope (K % 4 == 0 too).
 bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, const float *w, int64_t wsh, int n);
 hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
                                            int64_t wsh, int n, PackedView outw, float range, const uint32_t *bits,
-                                           const int *count, const uint64_t *lanenib, const uint16_t *lanerank,
-                                           const uint32_t *rowbits, float *xo, hipStream_t stream);
+                                           const int *count, const uint64_t *lanenib, const uint32_t *rowbits,
+                                           hipStream_t stream);
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
@@ -169,13 +168,12 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
                                int m, int n, float inv_r2, void *scratch, size_t scratch_bytes, hipStream_t stream,
                                const float *bias = nullptr, bool relu = false, bool tickets_zeroed = false);
 // The LLM.int8() decomposition's GEMM: int8 part + the outlier columns' fp32 products in the epilogue, read from
-// xo [m][cnt] (X's outlier values, compact) and W (k x n, row stride wsh) at the rows ocols[0 .. cnt) (ascending),
-// cnt = *ocount.
+// X (m x k, row stride xsh) and W (k x n, row stride wsh) at the columns / rows ocols[0 .. *ocount) (ascending).
 // Only where the plan is the
 // 256-tile GEMM without split-K (gemm_outlier_ok); hipErrorNotSupported otherwise.
 bool gemm_outlier_ok(int m, int n, int k);
 hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b, float *C, int64_t csh, int m, int n,
-                                       float inv_r2, const float *xo, const float *w, int64_t wsh,
+                                       float inv_r2, const float *x, int64_t xsh, const float *w, int64_t wsh,
                                        const int *ocols, const int *ocount, hipStream_t stream);
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
                            hipStream_t stream);
