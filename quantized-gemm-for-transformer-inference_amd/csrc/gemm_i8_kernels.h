@@ -74,6 +74,8 @@ struct GemmArgs {
     int rot_rows;
     int64_t xo_ld;
     const int *ocols;
+    uint32_t *ozero;  // kEpiOutlier: workgroup 0 zeroes ozero[0 .. ozero_words) (the consumed flags accumulator)
+    int ozero_words;
 };
 
 // Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
@@ -230,6 +232,9 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     if constexpr (kEpi == kEpiOutlier) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) ocol[tt] = 4 * tt + (lane >> 4) < ocnt ? p.ocols[4 * tt + (lane >> 4)] : 0;
+        // the pack has read the flags accumulator: clean it for the next call (write-through, as the flags atomics are)
+        if (blockIdx.x == 0 && tid < p.ozero_words)
+            __hip_atomic_store(p.ozero + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     v4i acc[8][8];

@@ -42,7 +42,6 @@ __device__ uint32_t g_flags_acc[kTicketSlots * kAccWords];
 namespace {
 
 constexpr int kChunkRows = 64;     // rows per flags block
-constexpr int kLaneWords = 128;    // K <= 4096 (the fast path): the pack's per-lane mask tables are built
 constexpr int kFlagCols = 1024;    // columns per flags block (256 threads x 4)
 
 // AbsCompareLTEConstFunc (op_elemwise.cuh:296-304): 0 when a in [-b, b], else 1 (NaN -> 1)
@@ -57,7 +56,7 @@ __device__ __forceinline__ bool is_outlier(float a, float b) {
 template <int P, int kThreads>
 __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial, int nchunks, int nwords,
                                             uint32_t *__restrict__ bits, int *__restrict__ rank, int *__restrict__ idx,
-                                            int *wsum, int *base, uint32_t *sbits /* LDS, words < kLaneWords */) {
+                                            int *wsum, int *base) {
     constexpr int kWaves = kThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s = tid % P;
@@ -97,7 +96,6 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
         if (s == 0 && w < nwords) {
             bits[w] = word;
             rank[w] = below;
-            if (w < kLaneWords) sbits[w] = word;
             int j = 0;
             for (uint32_t b = word; b; b &= b - 1, ++j) idx[1 + below + j] = 32 * w + __builtin_ctz(b);
         }
@@ -119,18 +117,16 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
 // builds the column mask, ranks, list and count (build_index over the accumulator or the partial words) and
 // re-zeroes the counters and the accumulator for the next call -- no separate index launch.
 constexpr int kFlagThreads = 1024, kFlagGroups = 4, kGroupRows = kChunkRows / kFlagGroups;
-template <bool VEC, bool kAcc>
+template <bool VEC, bool kAcc, bool kIndex>
 __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float *__restrict__ X, int64_t xsh, int m,
                                                                      int k, float t, uint32_t *__restrict__ partial,
                                                                      int nwords, int slot, uint32_t *__restrict__ bits,
-                                                                     int *__restrict__ rank, int *__restrict__ idx,
-                                                                     uint64_t *__restrict__ lanenib,
-                                                                     uint32_t *__restrict__ rowbits) {
+                                                                     int *__restrict__ rank, int *__restrict__ idx) {
+    static_assert(kAcc || kIndex, "the partial words need the index build");
     unsigned *ticket = g_flags_ticket + slot * kTicketStride;  // counter x (x < 8: per XCD, 8: global) at x * 32
     uint32_t *acc = g_flags_acc + slot * kAccWords;
     __shared__ int wsum[kFlagThreads / 64];
     __shared__ uint32_t nibs[kFlagGroups - 1][256];
-    __shared__ uint32_t sbits[kLaneWords];
     __shared__ unsigned last;
     __shared__ int count;
     const int tid = threadIdx.x, ct = tid & 255, g = tid >> 8;
@@ -172,8 +168,10 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        if constexpr (!kIndex) return;  // the fast path: the masked pack reads the accumulator itself
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if constexpr (!kIndex) return;
     __syncthreads();
     if (tid == 0) {
         // blocks b, b + 8, ... share an XCD (round-robin dispatch); the last of each XCD arrives globally
@@ -193,37 +191,10 @@ __global__ __launch_bounds__(kFlagThreads) void outlier_flags_kernel(const float
     __syncthreads();
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the sc1 loads stay below
-    if constexpr (kAcc) build_index<1, kFlagThreads>(acc, 1, nwords, bits, rank, idx, wsum, &count, sbits);
-    else build_index<1, kFlagThreads>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count, sbits);
-    __syncthreads();  // every accumulator word has been read; sbits is complete
+    if constexpr (kAcc) build_index<1, kFlagThreads>(acc, 1, nwords, bits, rank, idx, wsum, &count);
+    else build_index<1, kFlagThreads>(partial, (int)gridDim.y, nwords, bits, rank, idx, wsum, &count);
+    __syncthreads();  // every accumulator word has been read
     if (tid == 0) idx[0] = count;
-    if (nwords <= kLaneWords) {
-        // the masked pack's tables (K <= 4096), one entry per thread: lanenib[l] nibble j = the mask nibble of X-row
-        // chunk c = l + 64 j (columns 4c .. 4c + 3: word c >> 3, shift 4 (c & 7)); rowbits[q] bit 4 i + e = W row
-        // 4 q + e + 1024 i
-        __shared__ uint32_t snib[64][2], srow[256];
-        if (tid < 128) snib[tid >> 1][tid & 1] = 0u;
-        if (tid < 256) srow[tid] = 0u;
-        __syncthreads();
-        {
-            const int l = tid & 63, j = tid >> 6;  // 1024 threads = 64 lanes x 16 chunks
-            const int c = l + 64 * j, w = c >> 3, sh = 4 * (c & 7);
-            const uint32_t wd = w < nwords ? sbits[w] : 0u;
-            const uint32_t nb = (wd >> sh) & 15u;
-            if (nb) atomicOr(&snib[l][j >> 3], nb << (4 * (j & 7)));
-            const int q = tid & 255, i = tid >> 8;  // 256 W-strip threads x 4 row blocks
-            uint32_t rb = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * q + e + 1024 * i;
-                if (r < k && ((sbits[r >> 5] >> (r & 31)) & 1u)) rb |= 1u << (4 * i + e);
-            }
-            if (rb) atomicOr(&srow[q], rb);
-        }
-        __syncthreads();
-        if (tid < 64) lanenib[tid] = (uint64_t)snib[tid][0] | ((uint64_t)snib[tid][1] << 32);
-        if (tid < 256) rowbits[tid] = srow[tid];
-    }
     if constexpr (kAcc)
         for (int i = tid; i < nwords; i += kFlagThreads)
             __hip_atomic_store(acc + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -282,8 +253,6 @@ int outlier_ticket_slot(hipStream_t s) {
 struct OutlierScratch {
     uint32_t *partial, *bits;
     int *rank, *idx;    // idx[0] = count, idx[1 ..] = the outlier columns ascending
-    uint64_t *lanenib;  // fast path: per-lane X-row chunk nibbles (64)
-    uint32_t *rowbits;  // fast path: per-thread W-strip row bits (256)
     float *xm, *wm;     // X' / W' (fallback)
     int nchunks, nwords;
 };
@@ -303,10 +272,6 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
     p += a256(sizeof(uint32_t) * v.nwords);
     v.rank = reinterpret_cast<int *>(p);
     p += a256(sizeof(int) * v.nwords);
-    v.lanenib = reinterpret_cast<uint64_t *>(p);
-    p += a256(sizeof(uint64_t) * 64);
-    v.rowbits = reinterpret_cast<uint32_t *>(p);
-    p += a256(sizeof(uint32_t) * 256);
     v.partial = reinterpret_cast<uint32_t *>(p);
     p += a256(sizeof(uint32_t) * (size_t)v.nchunks * v.nwords);
     v.xm = reinterpret_cast<float *>(p);
@@ -317,26 +282,43 @@ OutlierScratch scratch_view(void *scratch, int m, int k) {
 
 template <bool VEC>
 void launch_flags(hipStream_t s, const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v,
-                  int slot) {
+                  int slot, bool index) {
     const dim3 grid((unsigned)((k + kFlagCols - 1) / kFlagCols), (unsigned)v.nchunks);
-    // K <= 32 768: the accumulator (the last workgroup reads nwords words); else every chunk's partial words
-    if (v.nwords <= kAccWords)
-        outlier_flags_kernel<VEC, true><<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot, v.bits,
-                                                                      v.rank, v.idx, v.lanenib, v.rowbits);
-    else
-        outlier_flags_kernel<VEC, false><<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot,
-                                                                       v.bits, v.rank, v.idx, v.lanenib, v.rowbits);
+    // K <= 32 768: the accumulator (the last workgroup reads nwords words, or -- !index, the fast path -- the pack
+    // reads them itself); else every chunk's partial words
+    auto go = [&](auto kern) { kern<<<grid, kFlagThreads, 0, s>>>(X, xsh, m, k, t, v.partial, v.nwords, slot, v.bits,
+                                                                  v.rank, v.idx); };
+    if (v.nwords > kAccWords) go(outlier_flags_kernel<VEC, false, true>);
+    else if (index) go(outlier_flags_kernel<VEC, true, true>);
+    else go(outlier_flags_kernel<VEC, true, false>);
+}
+
+// the device address of the stream's accumulator slot (hipGetSymbolAddress once per device; not a stream operation)
+uint32_t *flags_acc(int slot) {
+    constexpr int kMaxDev = 64;
+    static uint32_t *base[kMaxDev];
+    static std::mutex mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!base[dev]) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_flags_acc)) != hipSuccess) return nullptr;
+        base[dev] = static_cast<uint32_t *>(p);
+    }
+    return base[dev] + (size_t)slot * kAccWords;
 }
 
 // column mask, ranks, index list and count of X's outlier columns: ONE launch (the last flags workgroup
 // builds the index)
-hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, hipStream_t s) {
+hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, const OutlierScratch &v, hipStream_t s,
+                        bool index = true) {
     const int slot = outlier_ticket_slot(s);
     if (slot < 0) return hipErrorOutOfMemory;  // more streams than ticket slots
     if (v.nchunks > 65535) return hipErrorNotSupported;
     const bool vec = (k % 4 == 0) && (xsh % 4 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
-    if (vec) launch_flags<true>(s, X, xsh, m, k, t, v, slot);
-    else launch_flags<false>(s, X, xsh, m, k, t, v, slot);
+    if (vec) launch_flags<true>(s, X, xsh, m, k, t, v, slot, index);
+    else launch_flags<false>(s, X, xsh, m, k, t, v, slot, index);
     return hipGetLastError();
 }
 
@@ -345,7 +327,6 @@ hipError_t outlier_scan(const float *X, int64_t xsh, int m, int k, float t, cons
 size_t outlier_scratch_bytes(int m, int n, int k) {
     const size_t nchunks = (size_t)(m + kChunkRows - 1) / kChunkRows, nwords = (size_t)(k + 31) / 32;
     return a256(sizeof(uint32_t) * nchunks * nwords) + a256(sizeof(uint32_t) * nwords) + a256(sizeof(int) * nwords) +
-           a256(sizeof(uint64_t) * 64) + a256(sizeof(uint32_t) * 256) +
            a256(sizeof(int) * ((size_t)k + 1)) + a256(sizeof(float) * (size_t)m * k) +
            a256(sizeof(float) * (size_t)k * (size_t)round_up(n, 256));
 }
@@ -355,19 +336,21 @@ size_t outlier_scratch_bytes(int m, int n, int k) {
 hipError_t outlier_fast(const float *X, const float *W, float *O, int m, int n, int k, float t, void *scratch,
                         PackedView va, PackedView vb, float range, hipStream_t s) {
     if (!gemm_outlier_ok(m, n, (int)va.k_pad) || !pack_single_pass_outlier_ok(X, k, m, k, W, n, n)) return hipErrorNotSupported;
-    // the lane tables are read as 8-B words: a scratch that is not 16-B aligned takes the materialising fallback
-    // before anything is enqueued
-    if (reinterpret_cast<uintptr_t>(scratch) % 16 != 0) return hipErrorNotSupported;
     const OutlierScratch v = scratch_view(scratch, m, k);
-    hipError_t e = outlier_scan(X, k, m, k, t, v, s);
+    const int slot = outlier_ticket_slot(s);
+    uint32_t *acc = slot < 0 ? nullptr : flags_acc(slot);
+    if (!acc || v.nwords > 128) return hipErrorNotSupported;  // nothing enqueued yet: the fallback runs
+    // flags: the mask words ORed into the stream's accumulator, no index; the masked pack reads the words itself and
+    // its workgroup 0 writes the count and column list; the GEMM's workgroup 0 zeroes the accumulator after them
+    hipError_t e = outlier_scan(X, k, m, k, t, v, s, /*index=*/false);
     if (e != hipSuccess) return e;
-    e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, v.bits, v.idx, v.lanenib, v.rowbits, s);
+    e = launch_pack_single_pass_outlier(X, k, m, k, va, W, n, n, vb, range, acc, v.nwords, v.idx, s);
     if (e == hipErrorNotSupported) return hipErrorUnknown;  // scan already enqueued: the envelope checks above disagree
     if (e != hipSuccess) return e;
     const float inv_r2 = 1.0f / (range * range);
     // the fp32 chain reads the outlier columns of X and rows of W where they lie (the column list idx + 1); a compact
     // copy of X's outlier values written by the pack measured slower (profiles/r05_maskpack_lab_xo_staged.log)
-    return launch_gemm_dequant_outlier(va, vb, O, n, m, n, inv_r2, X, k, W, n, v.idx + 1, v.idx, s);
+    return launch_gemm_dequant_outlier(va, vb, O, n, m, n, inv_r2, X, k, W, n, v.idx + 1, v.idx, acc, v.nwords, s);
 }
 
 // Fallback phase 1: flags, indices, X', W' into scratch; the caller then runs the int8 chain on (X', W')

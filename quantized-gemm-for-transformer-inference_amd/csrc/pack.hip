@@ -127,15 +127,39 @@ __device__ __forceinline__ void zero_words_block0(uint32_t *words, int n) {
 // column when bit k of `bits` is set.  The int8 chain runs on X' / W' = X / W with those columns /
 // rows zeroed, so the packs treat them as +0 (absmax candidates, the signed seed and the quantized
 // bytes alike, exactly as packing the zeroed copies).  The fp32 part reads the original values from X and W
-// themselves (gemm_i8_fm<kEpiOutlier>), so nothing is written here.  The flags launch lays the mask out per
-// lane: lanenib[l] nibble j = the bits of X-row chunk l + 64 j (columns 4 (l + 64 j) .. +3), rowbits[q] bit
-// 4 i + e = W row 4 q + e + 1024 i -- one load per lane or thread, no shuffles.
+// themselves (gemm_i8_fm<kEpiOutlier>), so nothing is written here but the column index.  The mask is the flags
+// launch's accumulator (outlier.hip: nwords <= 128 words, bit c of word w = column 32 w + c), read by every
+// thread for exactly the words of its own elements, issued ahead of its data: an X-row lane's chunk l + 64 j
+// (columns 4 (l + 64 j) .. +3) is nibble l & 7 of word (l >> 3) + 8 j, a W-strip thread's rows 4 q + e + 1024 i
+// are bits of word (4 q + 1024 i) >> 5.  Workgroup 0 also builds the column count and the ascending list for the
+// GEMM (idx[0], idx[1 ..]).
 struct OutlierMask {
-    const uint32_t *bits;      // ceil(K/32) words (bit 0 of word 0: column 0, the absmax seed)
-    const int *count;          // outlier columns (device)
-    const uint64_t *lanenib;   // 64 lanes
-    const uint32_t *rowbits;   // 256 W-strip thread rows
+    const uint32_t *acc;  // nwords mask words (bit 0 of word 0: column 0, the absmax seed)
+    int nwords;
+    int *idx;             // out: [count][columns ascending]
 };
+// workgroup 0 of the masked pack: idx[0] = the outlier columns, idx[1 ..] = them ascending (nwords <= blockDim)
+__device__ __forceinline__ void outlier_column_list(const OutlierMask &om, int *wsum /* LDS, blockDim / 64 */) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nwave = blockDim.x >> 6;
+    const uint32_t word = t < om.nwords ? om.acc[t] : 0u;
+    const int pc = __popc(word);
+    int x = pc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(x, off, 64);
+        if (lane >= off) x += v;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int below = x - pc, total = 0;
+    for (int j = 0; j < nwave; ++j) {
+        below += j < wave ? wsum[j] : 0;
+        total += wsum[j];
+    }
+    int j = 0;
+    for (uint32_t b = word; b; b &= b - 1, ++j) om.idx[1 + below + j] = 32 * t + __builtin_ctz(b);
+    if (t == 0) om.idx[0] = total;
+}
 
 // ------------------------------------------------------------------------------------------------
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
@@ -174,11 +198,16 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         // buffer loads on one per-lane offset; chunks >= nfull lie past the descriptor and read as zeros
         typedef int v4i_t __attribute__((ext_vector_type(4)));
         const auto rs = buf_rsrc(srow, (uint32_t)nfull * 16);
-        // the lane's mask nibbles (16 chunks), issued ahead of the row so that they arrive with it
-        uint64_t ln = 0;
+        // the lane's mask words (chunk lane + 64 j: word (lane >> 3) + 8 j), issued ahead of the row so that they
+        // arrive with it
+        uint32_t mwd[R > 0 ? R : 1];
         if constexpr (kMask) {
-            static_assert(R <= 16, "the lane table covers len <= 4096");
-            ln = om->lanenib[lane];
+            static_assert(R <= 16, "the mask words cover len <= 4096");
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int w = (lane >> 3) + 8 * j;
+                mwd[j] = w < om->nwords ? om->acc[w] : 0u;
+            }
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -187,11 +216,11 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         }
         if constexpr (kMask) {
             // outlier columns: X' holds +0 there (the seed included); branch-free selects
-            if (*om->count > 0) {
-                if (om->bits[0] & 1u) seed = 0.0f;
+            {
+                if (om->acc[0] & 1u) seed = 0.0f;
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    const uint32_t nib = (uint32_t)(ln >> (4 * j)) & 15u;
+                    const uint32_t nib = (mwd[j] >> (4 * (lane & 7))) & 15u;
                     v[j].x = (nib & 1u) ? 0.0f : v[j].x;
                     v[j].y = (nib & 2u) ? 0.0f : v[j].y;
                     v[j].z = (nib & 4u) ? 0.0f : v[j].z;
@@ -974,9 +1003,15 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     const float w_seed = t < kWs8Cols ? w[n0 + t] : 0.0f;  // W[0, j], issued first (used after the reduction)
     const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kWs8Cols) * 4));
     const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c2) * 4);
-    // the thread's mask bits (its 16 rows), issued ahead of the strip's loads
-    uint32_t rb = 0;
-    if constexpr (kMask) rb = om->rowbits[rq];
+    // the mask words of the thread's rows (4 rq + e + 1024 i: word (4 rq + 1024 i) >> 5), issued ahead of the strip's
+    // loads
+    uint32_t mw[4] = {0u, 0u, 0u, 0u};
+    if constexpr (kMask)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = (4 * rq + 1024 * i) >> 5;
+            mw[i] = w < om->nwords ? om->acc[w] : 0u;
+        }
     float4 v[4][4];  // [i][e]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -988,13 +1023,14 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     bool seed_masked = false;
     if constexpr (kMask) {
         // outlier rows of W (outlier feature columns of X): W' holds +0 there; branch-free selects
-        if (*om->count > 0) {
-            seed_masked = om->bits[0] & 1u;
+        {
+            seed_masked = om->acc[0] & 1u;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const bool z = (rb >> (4 * i + e)) & 1u;
+                    const int r = 4 * rq + e + 1024 * i;
+                    const bool z = r < k && ((mw[i] >> (r & 31)) & 1u);
                     v[i][e].x = z ? 0.0f : v[i][e].x;
                     v[i][e].y = z ? 0.0f : v[i][e].y;
                     v[i][e].z = z ? 0.0f : v[i][e].z;
@@ -1097,6 +1133,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kWavesPerEu
         const int xcd = bid & 7, q8 = nstrips >> 3, r8 = nstrips & 7;
         const int strip = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
         pack_w_strip8_body<kMask>(strip, w, wsh, k, range, w_scale, w_q, k_pad, red, &om);
+        if constexpr (kMask)
+            if (bid == 0) {
+                __syncthreads();  // red is reused as the scan's wave sums
+                outlier_column_list(om, reinterpret_cast<int *>(red));
+            }
     } else if (bid < nstrips + npad) {
         const int64_t n0 = n + (int64_t)(bid - nstrips) * kWs8Cols;
         zero_packed_rows(w_q, n0, kWs8Cols, k_pad, threadIdx.x, 512);
@@ -1272,14 +1313,14 @@ bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, cons
 }
 
 hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *bits,
-                                           const int *count, const uint64_t *lanenib, const uint32_t *rowbits,
-                                           hipStream_t stream) {
+                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *acc,
+                                           int nwords, int *idx, hipStream_t stream) {
     if (!pack_single_pass_outlier_ok(x, xsh, m, k, w, wsh, n)) return hipErrorNotSupported;
     const int nstrips = n / kWs8Cols;
     const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
     const int nx = (int)(outx.rows_pad / 8);
-    const OutlierMask om{bits, count, lanenib, rowbits};
+    if (nwords > 128) return hipErrorNotSupported;  // K <= 4096, the single pass's envelope
+    const OutlierMask om{acc, nwords, idx};
     // a 4-waves-per-SIMD register budget (102 VGPRs, the same two blocks per CU): at 5 the masked body spilled
     // 20 B per lane (profiles/r03_ab_maskpack_wpe.log)
     pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(
