@@ -6,6 +6,8 @@
 //   the kernel, 2: + 8 x wave, 3: + 16 x wm, 4: (13 tn + 5 tm), 5: tn + 8 tm, 6: + 16 x wn -- FFN up 117.0-118.4
 //   vs 117.8 us for rot 1 and 122.3 unrotated, the shard 114.4-115.6 for all (profiles/r04_rot_variants_lab.log):
 //   nothing better than the product's order, so the switch was removed; this harness now compares 0 and 1.
+//   Round 5: gemm_i8_fm stores from registers and the field is GemmArgs::wide_rows (paired nontemporal stores at 0,
+//   plain per-tile stores at 1); the rotation is gone (lab/gemm_ds.h), so rot 1 here now means wide-row stores.
 //   build/rot_lab [rounds]
 #include <cstdio>
 #include <cstdlib>
@@ -47,7 +49,7 @@ int main(int argc, char **argv) {
         auto gemm = [&](int rot) {
             GemmArgs p{};
             p.A = A; p.B = B; p.Cx = Cx; p.Cw = Cw; p.C = C; p.csh = n; p.csw = 1; p.m = m; p.n = n; p.k_pad = k;
-            p.tiles_m = m / 256; p.tiles_n = n / 256; p.inv_r2 = 1.0f / (127.f * 127.f); p.splits = 1; p.rot_rows = rot;
+            p.tiles_m = m / 256; p.tiles_n = n / 256; p.inv_r2 = 1.0f / (127.f * 127.f); p.splits = 1; p.wide_rows = rot;
             gemm_i8_fm<kEpiNone><<<p.tiles_m * p.tiles_n, 256>>>(p);
         };
         std::vector<float> ref((size_t)m * n), got(ref.size());

@@ -104,7 +104,7 @@ int main(int argc, char **argv) {
         GemmArgs q = p;
         if (v.kind == 1) { q.splits = 2; q.slabs = slabs; q.tickets = tickets; q.reset_tickets = 1; }
         if (v.kind == 2) q.tiles_n = n / 128;
-        if (v.kind == 3) q.rot_rows = 1;
+        if (v.kind == 3) q.wide_rows = 1;
         return q;
     };
     auto grid_of = [&](const Variant &v) { return dim3(v.kind == 1 || v.kind == 2 ? nb * 2 : nb); };

@@ -95,7 +95,7 @@ int main(int argc, char **argv) {
         gemm::GemmArgs p{};
         p.A = vx.q; p.B = vw.q; p.Cx = vx.scale; p.Cw = vw.scale; p.C = C; p.csh = n; p.csw = 1; p.m = m; p.n = n;
         p.k_pad = vx.k_pad; p.tiles_m = tiles_m; p.tiles_n = tiles_n; p.inv_r2 = 1.0f / (127.f * 127.f); p.splits = 1;
-        p.rot_rows = n >= 16384 ? 1 : 0;
+        p.wide_rows = n >= 16384 ? 1 : 0;
         gemm::gemm_i8_fm<gemm::kEpiNone><<<tiles_m * tiles_n, 256, 0, s0>>>(p);
     };
     // outputs: the nt pack writes the same bytes

@@ -173,8 +173,10 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, csw, m, n, a.k_pad, g.tiles_m, g.tiles_n,
                inv_r2, 1, nullptr, nullptr, bias, tickets_zeroed ? 1 : 0};
     const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
-    // output rows of >= 64 KiB (FFN up's 16 384 columns): rotate each 256-tile's row-store order (gemm_i8_fm)
-    p.rot_rows = (csw == 1 && csh >= 16384) ? 1 : 0;
+    // output rows of >= 64 KiB (FFN up's 16 384 columns): gemm_i8_fm's LDS-image stores (512-B nontemporal row
+    // segments, rotated per tile); its paired nontemporal register stores ran 122.6 vs 112.3 us there
+    // (lab/ds_lab.hip) and plain ones left the output in the caches
+    p.wide_rows = (csw == 1 && csh >= 16384) ? 1 : 0;
     if (g.splits > 1 && scratch && scratch_bytes >= gemm_scratch_bytes(m, n, (int)a.k_pad)) {
         p.splits = g.splits;
         p.tickets = static_cast<unsigned *>(scratch);
@@ -221,6 +223,7 @@ hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b,
     const GemmPlan g = gemm_plan(m, n, (int)a.k_pad);
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, 1, m, n, a.k_pad, g.tiles_m, g.tiles_n,
                inv_r2, 1, nullptr, nullptr, nullptr, 0, x, w, ocount, wsh};
+    p.wide_rows = csh >= 16384 ? 1 : 0;
     p.xo_ld = xsh;
     p.ocols = ocols;
     p.ozero = ozero;

@@ -69,9 +69,9 @@ struct GemmArgs {
     const float *wo;
     const int *ocount;
     int64_t wo_ld;
-    // gemm_i8_fm's full-tile stores: each tile starts its row-pair loop at its own offset (set by the host for
-    // output rows of >= 64 KiB, where the tiles' concurrent row writes otherwise meet on the same memory channels)
-    int rot_rows;
+    // gemm_i8_fm's full-tile stores for output rows of >= 64 KiB (set by the host): through a per-wave LDS image as
+    // 512-B row segments in a per-tile rotated order; narrower rows take the paired register stores (see gemm_i8_fm)
+    int wide_rows;
     int64_t xo_ld;
     const int *ocols;
     uint32_t *ozero;  // kEpiOutlier: workgroup 0 zeroes ozero[0 .. ozero_words) (the consumed flags accumulator)
@@ -155,8 +155,17 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs &p, unsigned *last
 // while u+1 and u+2 are in flight (hipcc's counted vmcnt waits).  The two waves that share an A (B) half
 // read the same blocks (L1).  Measured against the ping-pong kernel (lab/w4_lab.hip, 4096^3, 5 boxes, bit-
 // identical): 58.3-62.3 vs 62.7-64.9 us; its main loop holds 1.90-1.97 GHz (no LDS traffic) vs 1.77-1.83.
-// Epilogue: per wave, two steps of 64 rows of its quadrant dequantized (scales in registers) into its OWN
-// padded [64][132] LDS block and stored from there as 512-B row segments: no cross-wave hand-off.
+// The MFMAs take the W fragment as their first operand and the X fragment as their second, so each accumulator
+// tile is C^T: lane (kq = lane >> 4, c = lane & 15) of tile (mi, ni) holds C[row 16 mi + c][columns 16 ni + 4 kq
+// .. + 3] -- four consecutive columns of one row.  The epilogue dequantizes on packed f32 pairs (v_pk_mul_f32 /
+// v_pk_add_f32: the scalar roundings, two elements per instruction) and stores from registers, no LDS image:
+// rows < 64 KiB exchange tiles ni, ni + 1 between lanes c and c ^ 8 (DPP row_ror:8) so one nontemporal store writes
+// 8 rows x 128 B; wider rows (FFN up) go through a per-wave LDS image (one 16-B write per tile and lane) and leave as
+// nontemporal 512-B row segments, each tile in its own rotated row order.  Lab (lab/ds_lab.hip,
+// profiles/r05_ds_lab.log, same box, interleaved, bit-identical): 4096^3 57.76 -> 56.30 us (round-4 LDS epilogue ->
+// paired register stores), the 8192-row shard 112.0 -> 110.0; FFN up's LDS image 120.45 vs 119.64 for round 4 (plain
+// register stores ran 112.3 there but left the output in the caches: the whole call -6.4 %, profiles/
+// r05_ab_epilogue.log).  The store tail is HBM-bound: the epilogue's arithmetic alone ends 1.7 us after the loop.
 // kI32: the raw int32 accumulators (qgemm_mm_packed_i32) instead of the dequantized fp32.
 __device__ __forceinline__ void mfma_agpr(v4i &acc, const v4i &a, const v4i &b) {
     asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
@@ -185,16 +194,18 @@ constexpr int kFmThreads = 256;
 //                 block that is not running: the first arriver has already drawn its ticket.
 enum SplitMode { kSplitNone = 0, kSplitFirst = 2 };
 
-// kNtC: the full-tile output stores are nontemporal (C2 bench, one box, interleaved: 11 598 vs 11 431 GEMMs/s, GEMM
-// 58.2 vs 59.5 us by events; profiles/r03_ab_nt_c.log) -- the 64-MiB tail streams past the caches
+// kNtC: the paired full-tile output stores (rows < 64 KiB) are nontemporal -- the 64-MiB tail streams past the
+// caches (lab/ds_lab.hip: dsPn 56.30 vs plain pairs 56.99 us at 4096^3; at >= 64-KiB rows nontemporal stores ran
+// 122.6 vs 112.3 us, hence plain there)
 template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
     static_assert(!(kEpi == kEpiOutlier && kSplit), "the outlier epilogue runs on unsplit plans");
-    constexpr int TS = 132;                 // padded row of a wave's epilogue block (conflict-free ds_write)
-    constexpr int kBlockBytes = 64 * TS * 4;
-    __shared__ __attribute__((aligned(16))) int8_t lds[4 * kBlockBytes + 2048 + 16];
+    // the one LDS array: the tile's scales (Cx of its 256 rows, Cw of its 256 columns), the split-K ticket word,
+    // then (wide rows) each wave's padded [64][TS] image of half its quadrant
+    constexpr int TS = 132;  // padded image row (16-B aligned, conflict-free 16-B writes of 16 rows)
+    __shared__ __attribute__((aligned(16))) float sS[2 * BM + 4 + 4 * 64 * TS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -225,6 +236,10 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         const_cast<int8_t *>(uniform_ptr(p.B + (((int64_t)tn * 16 + wn * 8) * nsub + u0) * 1024)), 0,
         __builtin_amdgcn_readfirstlane(half_bytes), 0x00020000);
     const int voff = lane * 16;
+    const int gi0 = tm * BM, gj0 = tn * BN;
+    // the scales are loaded first (scales are padded to the 256-row tiles): their latency hides under the operand
+    // prologue, and they reach LDS before the k-loop
+    const float sx = kI32 ? 0.0f : p.Cx[gi0 + tid], sw = kI32 ? 0.0f : p.Cw[gj0 + tid];
     // kEpiOutlier: the outlier-column count (device-side) and the lane's columns of the first two f32-MFMA steps
     // (t = 4 tt + kq), read before the k-loop so the epilogue's operand loads do not wait on them
     const int ocnt = kEpi == kEpiOutlier ? __builtin_amdgcn_readfirstlane(*p.ocount) : 0;
@@ -259,7 +274,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni) mfma_agpr(acc[mi][ni], ca[mi], cb[ni]);
+            for (int ni = 0; ni < 8; ++ni) mfma_agpr(acc[mi][ni], cb[ni], ca[mi]);  // W first: the tile comes out C^T
             if (more) {
                 ld(na, nb, 2 * mi, un);
                 ld(na, nb, 2 * mi + 1, un);
@@ -270,6 +285,8 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     };
 #pragma unroll
     for (int j = 0; j < 16; ++j) ld(a0, b0, j, 0);
+    sS[tid] = sx;
+    sS[BM + tid] = sw;
 #pragma unroll
     for (int j = 0; j < 16; ++j) ld(a1, b1, j, nloc > 1 ? 1 : 0);
     int u = 0;
@@ -286,7 +303,7 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     // the last MFMAs' results are read by VALU below; the asm statements hide them from hipcc's padding
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     if constexpr (kSplit == kSplitFirst) {
-        unsigned *last = reinterpret_cast<unsigned *>(lds + 4 * kBlockBytes + 2048);
+        unsigned *last = reinterpret_cast<unsigned *>(sS + 2 * BM);
         if (tid == 0) *last = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if (*last == 0u) {
@@ -311,57 +328,56 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
                 __builtin_amdgcn_s_sleep(2);
             if (p.reset_tickets) __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: slab loads stay below
     }
+    __syncthreads();  // the scale image (and the split-K hand-off above)
 
-    const int gi0 = tm * BM, gj0 = tn * BN;
-    const int lrow = lane & 15, kq = lane >> 4;
+    // lane (kq, c) of tile (mi, ni): row 16 mi + c, columns 16 ni + 4 kq .. + 3 of the wave's 128 x 128 quadrant
+    const int c = lane & 15, kq = lane >> 4;
     const int r0 = wm * 128, c0 = wn * 128;
-    // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) for both halves, loaded
-    // together here so their latency is paid once: ow[step][ni] = W[col_t][j], ox[half][mq][step] = X[row][col_t]
-    // with t = 4 step + kq; +0 / -0 past the count (see below)
-    float ox[2][4][2], ow[2][8];
+    // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) for every row block, loaded
+    // together here so their latency is paid once: ow[step][ni] = W[col_t][j] (j = 16 ni + c), ox[mi][step] =
+    // X[row 16 mi + c][col_t], t = 4 step + kq; +0 / -0 past the count (see below)
+    float ox[8][2], ow[2][8];
     if constexpr (kEpi == kEpiOutlier) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
             const int t = 4 * tt + kq;
 #pragma unroll
             for (int ni = 0; ni < 8; ++ni) {
-                const int j = gj0 + c0 + ni * 16 + lrow;
+                const int j = gj0 + c0 + ni * 16 + c;
                 ow[tt][ni] = t < ocnt ? (j < p.n ? p.wo[(int64_t)ocol[tt] * p.wo_ld + j] : 0.0f) : -0.0f;
             }
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int mq = 0; mq < 4; ++mq) {
-                    const int i = gi0 + r0 + 64 * h + mq * 16 + lrow;
-                    ox[h][mq][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * p.xo_ld + ocol[tt]] : 0.0f;
-                }
+            for (int mi = 0; mi < 8; ++mi) {
+                const int i = gi0 + r0 + 16 * mi + c;
+                ox[mi][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * p.xo_ld + ocol[tt]] : 0.0f;
+            }
         }
     }
-    float *sCx = reinterpret_cast<float *>(lds + 4 * kBlockBytes);
-    float *sCw = sCx + BM;
-    if constexpr (!kI32) {
-        sCx[tid] = p.Cx[gi0 + tid];  // scales are padded to the 256-row tiles
-        sCw[tid] = p.Cw[gj0 + tid];
-    }
-    __syncthreads();
-    float *T = reinterpret_cast<float *>(lds + wave * kBlockBytes);
-    const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
-                      gj0 + BN <= p.n && gi0 + BM <= p.m;
-    // row-pair rotation of the full-tile stores (lab/w4_lab.hip `stride` mode, profiles/r03_f4_store_order_lab.log:
-    // FFN-up output, 64-KiB rows, 121.6 -> 118.2 us; at 16-KiB rows it cost the 8192-row shard 2 us, hence host-set)
-    const int rot = __builtin_amdgcn_readfirstlane(p.rot_rows ? ((tn * 7 + tm * 3) & 31) : 0);
-    // the scales (and bias) into registers first: T and the scales share the one LDS array, so a scale read
-    // between T stores would be re-issued and waited for after every store
-    float cwv[8], bv[8];
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    // the scales (and bias) into registers
+    float cx[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) cx[mi] = sS[r0 + 16 * mi + c];
+    v4f cw[8], bv[8];
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) {
-        cwv[ni] = kI32 ? 0.0f : sCw[c0 + ni * 16 + lrow];
-        const int j = gj0 + c0 + ni * 16 + lrow;
-        bv[ni] = has_bias(kEpi) && j < p.n ? p.bias[j] : 0.0f;
+        cw[ni] = *reinterpret_cast<const v4f *>(sS + BM + c0 + 16 * ni + 4 * kq);
+        const int j = gj0 + c0 + 16 * ni + 4 * kq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[ni][r] = has_bias(kEpi) && j + r < p.n ? p.bias[j + r] : 0.0f;
     }
+    const v2f inv2 = {p.inv_r2, p.inv_r2};
+    const v2f zero2 = {0.0f, 0.0f};
+    float *C = static_cast<float *>(p.C);
+    const bool full = p.csw == 1 && (p.csh % 4 == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0) &&
+                      gj0 + BN <= p.n && gi0 + BM <= p.m;
+    const bool pairs = full && !p.wide_rows;
+    const bool image = full && p.wide_rows;
+    const bool lo = c < 8;
+    float *T = sS + 2 * BM + 4 + wave * 64 * TS;  // this wave's image (wide rows)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         // split-K reducer: the other slice's partial sums of this half (32 sc1 loads in flight, then the adds)
@@ -378,32 +394,26 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
                     oth[mq][ni] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + ((4 * s + mq) * 8 + ni) * 1024,
                                                                         0, 16 /* sc1 */);
         }
-        float cxv[4][4];
 #pragma unroll
-        for (int mq = 0; mq < 4; ++mq)
+        for (int mq = 0; mq < 4; ++mq) {
+            const int mi = 4 * s + mq;
+            // kEpiOutlier: Co = the fp32 chain over the outlier columns from +0 in ascending t of xo[i][t] *
+            // wo[t][j], on v_mfma_f32_16x16x4_f32 (its result is that k-ordered chain bit for bit, as in the fp32
+            // GEMMs): 4 columns per MFMA, W first so D is laid out as the int32 accumulators, one 16-row block at a
+            // time.  A step past the count multiplies -0 by +0: fma(-0, +0, c) = c for every c, -0 included (+0 *
+            // +0 would turn a -0 sum into +0).  The first 8 columns' operands were loaded once (ox / ow); columns
+            // past 8 load per step.
+            v4f oc[8];
+            if constexpr (kEpi == kEpiOutlier) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cxv[mq][r] = kI32 ? 0.0f : sCx[r0 + 64 * s + mq * 16 + 4 * kq + r];
-        if constexpr (kEpi == kEpiOutlier) {
-            // O = fl(O8 + Co), Co = the fp32 chain over the outlier columns from +0 in ascending t of
-            // xo[i][t] * wo[t][j], on v_mfma_f32_16x16x4_f32 (its result is that k-ordered chain bit for bit,
-            // as in the fp32 GEMMs): 4 columns per MFMA, D laid out as the int32 accumulators, one 16-row
-            // block of the half at a time.  A step past the count multiplies +0 by -0: fma(+0, -0, c) = c for
-            // every c, -0 included (+0 * +0 would turn a -0 sum into +0).
-            // The first 8 columns' operands were loaded once, ahead of both halves (ox / ow); columns past 8
-            // load per step.
-            typedef float v4f_t __attribute__((ext_vector_type(4)));
-#pragma unroll
-            for (int mq = 0; mq < 4; ++mq) {
-                v4f_t oc[8];
-#pragma unroll
-                for (int ni = 0; ni < 8; ++ni) oc[ni] = v4f_t{0.f, 0.f, 0.f, 0.f};
+                for (int ni = 0; ni < 8; ++ni) oc[ni] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int tt = 0; tt < 2; ++tt)
                     if (4 * tt < ocnt)
 #pragma unroll
                         for (int ni = 0; ni < 8; ++ni)
-                            oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(ox[s][mq][tt], ow[tt][ni], oc[ni], 0, 0, 0);
-                const int ia = gi0 + r0 + 64 * s + mq * 16 + lrow;  // the A-operand row of this lane
+                            oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(ow[tt][ni], ox[mi][tt], oc[ni], 0, 0, 0);
+                const int ia = gi0 + r0 + 16 * mi + c;  // the B-operand row (X row) of this lane
 #pragma unroll 1
                 for (int t0 = 8; t0 < ocnt; t0 += 4) {
                     const int t = t0 + kq;  // the lane's k within the MFMA step
@@ -412,71 +422,89 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
                     float wb[8];
 #pragma unroll
                     for (int ni = 0; ni < 8; ++ni) {
-                        const int j = gj0 + c0 + ni * 16 + lrow;
+                        const int j = gj0 + c0 + ni * 16 + c;
                         wb[ni] = t < ocnt ? (j < p.n ? p.wo[(int64_t)col * p.wo_ld + j] : 0.0f) : -0.0f;
                     }
 #pragma unroll
-                    for (int ni = 0; ni < 8; ++ni) oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, wb[ni], oc[ni], 0, 0, 0);
+                    for (int ni = 0; ni < 8; ++ni) oc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[ni], xa, oc[ni], 0, 0, 0);
                 }
-                // no outlier column (count 0, wave-uniform): O = O8 with no add, as the oracle (qgemm_oracle.c
-                // oracle_mm_outlier skips it) -- fl(-0 + +0) would turn an O8 of -0 into +0
-#pragma unroll
-                for (int ni = 0; ni < 8; ++ni)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float o8 = dequantize(acc[4 * s + mq][ni][r], outer_product(cxv[mq][r], cwv[ni]), p.inv_r2);
-                        T[(mq * 16 + 4 * kq + r) * TS + ni * 16 + lrow] = ocnt > 0 ? __fadd_rn(o8, oc[ni][r]) : o8;
-                    }
             }
-        } else {
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni) {
-            const int jl = ni * 16 + lrow;
-#pragma unroll
-            for (int mq = 0; mq < 4; ++mq)
+            // the four outputs of tile (mi, ni) in this lane: O = fl(fl(float(acc) * (fl(Cx * Cw) + 0)) * inv_r2) on
+            // packed pairs (-ffp-contract=off: no contraction), then the epilogue extras
+            auto tile_out = [&](int ni) __attribute__((always_inline)) -> v4f {
+                v4i a = acc[mi][ni];
+                if constexpr (kSplit) a += oth[mq][ni];
+                if constexpr (kI32) return v4f{__int_as_float(a[0]), __int_as_float(a[1]), __int_as_float(a[2]),
+                                               __int_as_float(a[3])};  // the raw bits
+                const v2f x = {cx[mi], cx[mi]};
+                const v2f o01 = x * v2f{cw[ni][0], cw[ni][1]} + zero2, o23 = x * v2f{cw[ni][2], cw[ni][3]} + zero2;
+                const v2f d01 = (v2f{(float)a[0], (float)a[1]} * o01) * inv2;
+                const v2f d23 = (v2f{(float)a[2], (float)a[3]} * o23) * inv2;
+                v4f o = {d01[0], d01[1], d23[0], d23[1]};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int il = mq * 16 + 4 * kq + r;
-                    float o;
-                    if constexpr (kI32) {
-                        o = __int_as_float(acc[4 * s + mq][ni][r]);  // the raw bits travel through LDS
-                    } else {
-                        const int a = kSplit ? acc[4 * s + mq][ni][r] + oth[mq][ni][r] : acc[4 * s + mq][ni][r];
-                        o = dequantize(a, outer_product(cxv[mq][r], cwv[ni]), p.inv_r2);
-                        if constexpr (has_bias(kEpi)) o = __fadd_rn(o, bv[ni]);
-                        if constexpr (kEpi == kEpiBiasRelu) o = (o < 0.0f) ? 0.0f : o;
-                    }
-                    T[il * TS + jl] = o;
+                    if constexpr (has_bias(kEpi)) o[r] = __fadd_rn(o[r], bv[ni][r]);
+                    if constexpr (kEpi == kEpiBiasRelu) o[r] = (o[r] < 0.0f) ? 0.0f : o[r];
+                    // no outlier column (count 0, wave-uniform): O = O8 with no add, as the oracle
+                    // (qgemm_oracle.c oracle_mm_outlier skips it) -- fl(-0 + +0) would turn an O8 of -0 into +0
+                    if constexpr (kEpi == kEpiOutlier) o[r] = ocnt > 0 ? __fadd_rn(o[r], oc[ni][r]) : o[r];
                 }
+                return o;
+            };
+            const int64_t row = gi0 + r0 + 16 * mi + c;
+#pragma unroll
+            for (int np = 0; np < 4; ++np) {
+                const v4f o0 = tile_out(2 * np), o1 = tile_out(2 * np + 1);
+                if (pairs) {
+                    // tiles 2 np and 2 np + 1 exchanged between lanes c and c ^ 8 (DPP row_ror:8): rows 16 mi + (c & 7)
+                    // take store 1, rows 16 mi + 8 + (c & 7) store 2, each 8 rows x 128 B
+                    v4f x1, x2;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float r0v = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(o0[e]), 0x128, 0xf, 0xf, false));
+                        const float r1v = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(o1[e]), 0x128, 0xf, 0xf, false));
+                        x1[e] = lo ? o0[e] : r1v;
+                        x2[e] = lo ? r0v : o1[e];
+                    }
+                    const int64_t ra = gi0 + r0 + 16 * mi + (c & 7);
+                    const int jc = gj0 + c0 + 32 * np + (lo ? 0 : 16) + 4 * kq;
+                    v4f *d1 = reinterpret_cast<v4f *>(C + ra * p.csh + jc);
+                    v4f *d2 = reinterpret_cast<v4f *>(C + (ra + 8) * p.csh + jc);
+                    if constexpr (kNtC) {
+                        __builtin_nontemporal_store(x1, d1);
+                        __builtin_nontemporal_store(x2, d2);
+                    } else {
+                        *d1 = x1;
+                        *d2 = x2;
+                    }
+                } else if (image) {
+                    *reinterpret_cast<v4f *>(T + (16 * mq + c) * TS + 32 * np + 4 * kq) = o0;
+                    *reinterpret_cast<v4f *>(T + (16 * mq + c) * TS + 32 * np + 16 + 4 * kq) = o1;
+                } else {
+                    const int j = gj0 + c0 + 32 * np + 4 * kq;  // tile 2 np; tile 2 np + 1 at j + 16
+                    if (row < p.m) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            if (j + e < p.n) C[row * p.csh + (int64_t)(j + e) * p.csw] = o0[e];
+                            if (j + 16 + e < p.n) C[row * p.csh + (int64_t)(j + 16 + e) * p.csw] = o1[e];
+                        }
+                    }
+                }
+            }
         }
-        }
-        // the wave's own block: its ds_writes precede its ds_reads (one wave's LDS ops stay in order)
-        const int c4 = (lane & 31) * 4;
-        float *C = static_cast<float *>(p.C);
-        if (full) {
+        if (image) {
+            // wide rows: the half's 64 rows read back from the wave's own image (one wave's LDS operations stay in
+            // order) and stored as 512-B row segments, nontemporal: plain stores there leave the 128-MiB FFN-up output
+            // in the caches and the next call's pack ran 15 us longer (same box, profiles/r05_ab_epilogue.log).  Each
+            // tile starts its row-pair loop at its own offset (its rows otherwise meet the other tiles' on the same
+            // memory channels; lab/rot_lab.hip, round 4: 122.3 -> 117.8 us)
+            const int rot = __builtin_amdgcn_readfirstlane((tn * 7 + tm * 3) & 31);
+            const int c4 = (lane & 31) * 4;
 #pragma unroll 8
             for (int it = 0; it < 32; ++it) {
                 const int rr = 2 * ((it + rot) & 31) + (lane >> 5);
-                const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
-                float4 *dst = reinterpret_cast<float4 *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4);
-                if constexpr (kNtC) {
-                    typedef float v4f __attribute__((ext_vector_type(4)));
-                    __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f *>(dst));
-                } else {
-                    *dst = v;
-                }
-            }
-        } else {
-            for (int it = 0; it < 32; ++it) {
-                const int rr = 2 * it + (lane >> 5);
-                const int i = gi0 + r0 + 64 * s + rr;
-                const float4 v = *reinterpret_cast<const float4 *>(T + rr * TS + c4);
-                const int j = gj0 + c0 + c4;
-                if (i >= p.m) continue;
-                const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (j + e < p.n) C[(int64_t)i * p.csh + (int64_t)(j + e) * p.csw] = vv[e];
+                const v4f v = *reinterpret_cast<const v4f *>(T + rr * TS + c4);
+                __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + c0 + c4));
             }
         }
     }
