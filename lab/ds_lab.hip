@@ -33,12 +33,15 @@ struct Variant {
     KernelFn fn;
     bool stamped = false;
     bool nostore = false;
-    bool rot = false;  // gemm_i8_fm's row-pair rotation (the product sets it for >= 64-KiB output rows)
+    bool rot = false;  // gemm_i8_fm's wide-row stores (the product sets them for >= 64-KiB output rows)
+    int outlier = -1;  // >= 0: gemm_i8_fm<kEpiOutlier> with this many outlier columns (not bit-checked against fm)
 };
 
 static Variant make(const std::string &spec) {
     if (spec == "fm") return {spec, gemm_i8_fm<>};
     if (spec == "fmrot") return {spec, gemm_i8_fm<>, false, false, true};  // product wide-row (LDS image) stores
+    if (spec == "fo0") { Variant v{spec, gemm_i8_fm<kEpiOutlier>, false, true}; v.outlier = 0; return v; }
+    if (spec == "fo8") { Variant v{spec, gemm_i8_fm<kEpiOutlier>, false, true}; v.outlier = 8; return v; }
     if (spec == "r4") return {spec, gemm_i8_fm_r4<>};
     if (spec == "r4w") return {spec, gemm_i8_fm_r4<>, false, false, true};
     if (spec == "ds") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsRowMajorOrder>};
@@ -83,6 +86,25 @@ int main(int argc, char **argv) {
     const int nb = p.tiles_m * p.tiles_n;
     dim3 grid(nb);
 
+    // outlier operands: X (m x k) and W (k x n) fp32, 8 ascending columns, the count per variant
+    float *Xo, *Wo; int *ocols, *ocnt;
+    CK(hipMalloc(&Xo, (size_t)m * k * 4)); CK(hipMalloc(&Wo, (size_t)k * n * 4));
+    CK(hipMalloc(&ocols, 64)); CK(hipMalloc(&ocnt, 4 * 16));
+    fill_f<<<4096, 256>>>(Xo, (int64_t)m * k, 5); fill_f<<<4096, 256>>>(Wo, (int64_t)k * n, 6);
+    {
+        int hc[8] = {5, 100, 1000, 2000, 2500, 3000, 3500, k - 1};
+        int hn[16] = {0, 8};
+        CK(hipMemcpy(ocols, hc, sizeof(hc), hipMemcpyHostToDevice));
+        CK(hipMemcpy(ocnt, hn, sizeof(hn), hipMemcpyHostToDevice));
+    }
+    auto vargs = [&](const Variant &v) {
+        GemmArgs q = p;
+        q.wide_rows = v.rot;
+        if (v.outlier >= 0) {
+            q.xo = Xo; q.xo_ld = k; q.wo = Wo; q.wo_ld = n; q.ocols = ocols; q.ocount = ocnt + (v.outlier ? 1 : 0);
+        }
+        return q;
+    };
     GemmArgs pr = p; pr.C = Cref;
     gemm_i8_fm<><<<grid, 256>>>(pr);
     CK(hipDeviceSynchronize());
@@ -106,7 +128,7 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 400; ++i) gemm_i8_fm<><<<grid, 256>>>(p);  // pre-warm the clocks
     for (int r = 0; r < rounds; ++r)
         for (size_t vi = 0; vi < vs.size(); ++vi) {
-            GemmArgs q = p; q.wide_rows = vs[vi].rot;
+            GemmArgs q = vargs(vs[vi]);
             for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, 256>>>(q);
             CK(hipEventRecord(e0));
             for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, 256>>>(q);
@@ -128,7 +150,7 @@ int main(int argc, char **argv) {
         float ms = 0;
         CK(hipEventRecord(e0));
         while (ms < 2000) {
-            for (int i = 0; i < 200; ++i) v.fn<<<grid, 256>>>(p);
+            for (int i = 0; i < 200; ++i) v.fn<<<grid, 256>>>(vargs(v));
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
         }
         std::vector<unsigned long long> st((size_t)nb * 4);

@@ -203,9 +203,11 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kSplit), "raw accumulators are not split");
     static_assert(!(kEpi == kEpiOutlier && kSplit), "the outlier epilogue runs on unsplit plans");
     // the one LDS array: the tile's scales (Cx of its 256 rows, Cw of its 256 columns), the split-K ticket word,
-    // then (wide rows) each wave's padded [64][TS] image of half its quadrant
+    // (wide rows) each wave's padded [64][TS] image of half its quadrant, (kEpiOutlier) the chain's operands
     constexpr int TS = 132;  // padded image row (16-B aligned, conflict-free 16-B writes of 16 rows)
-    __shared__ __attribute__((aligned(16))) float sS[2 * BM + 4 + 4 * 64 * TS];
+    constexpr int kOutlierStage = kEpi == kEpiOutlier ? 2 * 8 * BM : 0;
+    __shared__ __attribute__((aligned(16))) float sS[2 * BM + 4 + 4 * 64 * TS + kOutlierStage];
+    float *const sO = sS + 2 * BM + 4 + 4 * 64 * TS;  // [8][256] X values, then [8][256] W values
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -238,15 +240,27 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     const int voff = lane * 16;
     const int gi0 = tm * BM, gj0 = tn * BN;
     // the scales are loaded first (scales are padded to the 256-row tiles): their latency hides under the operand
-    // prologue, and they reach LDS before the k-loop
+    // prologue, and they reach LDS before the k-loop.  (LDS-DMA here instead makes hipcc wait for vmcnt(0) before
+    // the first MFMA: it orders the inline-asm MFMAs behind every pending LDS-DMA write.)
     const float sx = kI32 ? 0.0f : p.Cx[gi0 + tid], sw = kI32 ? 0.0f : p.Cw[gj0 + tid];
-    // kEpiOutlier: the outlier-column count (device-side) and the lane's columns of the first two f32-MFMA steps
-    // (t = 4 tt + kq), read before the k-loop so the epilogue's operand loads do not wait on them
+    // kEpiOutlier: the outlier-column count (device-side) and the operands of the chain's first 8 columns for this
+    // tile -- X[row][col_t] of its 256 rows, W[col_t][j] of its 256 columns, +0 / -0 past the count (see the
+    // epilogue) -- gathered first and staged in LDS after the operand prologue is in flight, so the epilogue reads
+    // them from LDS and never waits on their latency (X's columns come from HBM: the pack streamed X past the caches)
     const int ocnt = kEpi == kEpiOutlier ? __builtin_amdgcn_readfirstlane(*p.ocount) : 0;
-    int ocol[2] = {0, 0};
+    float oxv[8], owv[8];
     if constexpr (kEpi == kEpiOutlier) {
+        const int64_t i = gi0 + tid;
+        const int j = gj0 + tid;
+        // the column list through the constant address space: scalar loads (a vector load here would make every
+        // column's gather wait for the ones before it)
+        const __attribute__((address_space(4))) int *ocs = (const __attribute__((address_space(4))) int *)p.ocols;
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) ocol[tt] = 4 * tt + (lane >> 4) < ocnt ? p.ocols[4 * tt + (lane >> 4)] : 0;
+        for (int t = 0; t < 8; ++t) {
+            const int col = t < ocnt ? ocs[t] : 0;
+            oxv[t] = t < ocnt && i < p.m ? p.xo[i * p.xo_ld + col] : 0.0f;
+            owv[t] = t < ocnt ? (j < p.n ? p.wo[(int64_t)col * p.wo_ld + j] : 0.0f) : -0.0f;
+        }
         // the pack has read the flags accumulator: clean it for the next call (write-through, as the flags atomics are)
         if (blockIdx.x == 0 && tid < p.ozero_words)
             __hip_atomic_store(p.ozero + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -289,6 +303,13 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     sS[BM + tid] = sw;
 #pragma unroll
     for (int j = 0; j < 16; ++j) ld(a1, b1, j, nloc > 1 ? 1 : 0);
+    if constexpr (kEpi == kEpiOutlier) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            sO[t * BM + tid] = oxv[t];
+            sO[(8 + t) * BM + tid] = owv[t];
+        }
+    }
     int u = 0;
     for (; u + 3 <= nloc; u += 3) {
         substep(a0, b0, a2, b2, u + 2, true);
@@ -335,24 +356,17 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     // lane (kq, c) of tile (mi, ni): row 16 mi + c, columns 16 ni + 4 kq .. + 3 of the wave's 128 x 128 quadrant
     const int c = lane & 15, kq = lane >> 4;
     const int r0 = wm * 128, c0 = wn * 128;
-    // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) for every row block, loaded
-    // together here so their latency is paid once: ow[step][ni] = W[col_t][j] (j = 16 ni + c), ox[mi][step] =
-    // X[row 16 mi + c][col_t], t = 4 step + kq; +0 / -0 past the count (see below)
+    // kEpiOutlier: the operands of the first 8 outlier columns (two f32-MFMA steps) from the LDS stage:
+    // ow[step][ni] = W[col_t][j] (j = 16 ni + c), ox[mi][step] = X[row 16 mi + c][col_t], t = 4 step + kq
     float ox[8][2], ow[2][8];
     if constexpr (kEpi == kEpiOutlier) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
             const int t = 4 * tt + kq;
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni) {
-                const int j = gj0 + c0 + ni * 16 + c;
-                ow[tt][ni] = t < ocnt ? (j < p.n ? p.wo[(int64_t)ocol[tt] * p.wo_ld + j] : 0.0f) : -0.0f;
-            }
+            for (int ni = 0; ni < 8; ++ni) ow[tt][ni] = sO[(8 + t) * BM + c0 + 16 * ni + c];
 #pragma unroll
-            for (int mi = 0; mi < 8; ++mi) {
-                const int i = gi0 + r0 + 16 * mi + c;
-                ox[mi][tt] = t < ocnt && i < p.m ? p.xo[(int64_t)i * p.xo_ld + ocol[tt]] : 0.0f;
-            }
+            for (int mi = 0; mi < 8; ++mi) ox[mi][tt] = sO[t * BM + r0 + 16 * mi + c];
         }
     }
     typedef float v2f __attribute__((ext_vector_type(2)));
