@@ -21,7 +21,7 @@ timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline --no-error-stats
 grep -o '"value": [0-9.]*' $out/bench_c2_again.log | head -1
 timeout -k 10 200 lab/build/maskpack_lab 4096 4096 4096 7 > $out/maskpack.log 2>&1 || { tail $out/maskpack.log; exit 1; }
 cat $out/maskpack.log
-for cfg in c2_outlier; do
+for cfg in c2 c2_outlier; do
   CFG=$cfg timeout -k 10 400 bash scripts/pmc_bench.sh > $out/pmc_$cfg.log 2>&1 || { tail $out/pmc_$cfg.log; exit 1; }
   python3 scripts/summarize_pmc.py gpurun_out/pmc_bench/$cfg $out/pmc_$cfg.json 4096 4096 4096 > $out/pmc_$cfg.sum 2>&1 || exit 1
 done
