@@ -86,6 +86,23 @@ def test_linear_fused_bias_relu_bit_exact(qg, oracle, device, M, N, K, bias, rel
     assert_bits_equal(Y.cpu().numpy(), oracle.linear(X, W, b, relu), f"linear {M}x{N}x{K} b={bias} relu={relu}")
 
 
+@pytest.mark.parametrize("M,N,K,relu,splits", [(2048, 4096, 1024, True, 1),    # register-store pairs
+                                              (2048, 4096, 2048, False, 2),   # ticket-first split-K
+                                              (2048, 16384, 512, True, 1),    # >= 64-KiB rows: the LDS image
+                                              (2000, 4100, 1000, True, 1)])   # partial tiles
+def test_linear_fused_bias_relu_256_tiles(qg, oracle, device, M, N, K, relu, splits):
+    """gemm_i8_fm's bias / bias+relu epilogues (the encoder's shapes all take the small-tile kernels), every output
+    bit, on each of its store paths."""
+    import ctypes
+    tile = ctypes.c_int(0)
+    assert qg.load().qgemm_gemm_plan(M, N, K, ctypes.byref(tile), None) == splits and tile.value == 256
+    X, W = oracle.inputs(M, N, K, 93)
+    b = oracle.uniform((N,), 94)
+    pw = qg.pack_b(_dev(W, device))
+    Y = qg.linear(_dev(X, device), pw, bias=_dev(b, device), relu=relu)
+    assert_bits_equal(Y.cpu().numpy(), oracle.linear(X, W, b, relu), f"linear {M}x{N}x{K} relu={relu}")
+
+
 @pytest.mark.parametrize("seq,d,H,dff,blocks", [
     (6, 8, 4, 8, 2),          # the reference's own Encoder call (transformer.cu:171-178)
     (32, 64, 4, 128, 2),
