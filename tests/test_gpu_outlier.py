@@ -43,7 +43,8 @@ def test_outlier_decomposition_bit_exact(qg, oracle, device, M, N, K, cols):
 # absmax seed) and the last column
 @pytest.mark.parametrize("M,N,K,cols", [(2500, 4000, 132, [0, 1, 31, 32, 63, 131]),
                                         (2560, 4096, 1024, list(range(7, 1024, 37))),
-                                        (2560, 4000, 64, list(range(64)))])
+                                        (2560, 4000, 64, list(range(64))),
+                                        (512, 16384, 256, [3, 100, 255])])  # >= 64-KiB rows: the LDS-image stores
 def test_outlier_fast_path_bit_exact(qg, oracle, device, M, N, K, cols):
     X, W = _with_outliers(oracle, M, N, K, cols, 9)
     C, cnt = qg.mm_outlier(_dev(X, device), _dev(W, device), 6.0)
