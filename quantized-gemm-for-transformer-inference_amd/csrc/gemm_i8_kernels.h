@@ -205,9 +205,12 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     // the one LDS array: the tile's scales (Cx of its 256 rows, Cw of its 256 columns), the split-K ticket word,
     // (wide rows) each wave's padded [64][TS] image of half its quadrant, (kEpiOutlier) the chain's operands
     constexpr int TS = 132;  // padded image row (16-B aligned, conflict-free 16-B writes of 16 rows)
-    constexpr int kOutlierStage = kEpi == kEpiOutlier ? 2 * 8 * BM : 0;
+    // (kEpiOutlier) stage rows of OS floats: the 4 k-groups of a wave read rows t = 4 tt + kq at the same offsets,
+    // so a row stride of BM would put them on the same banks
+    constexpr int OS = BM + 16;
+    constexpr int kOutlierStage = kEpi == kEpiOutlier ? 2 * 8 * OS : 0;
     __shared__ __attribute__((aligned(16))) float sS[2 * BM + 4 + 4 * 64 * TS + kOutlierStage];
-    float *const sO = sS + 2 * BM + 4 + 4 * 64 * TS;  // [8][256] X values, then [8][256] W values
+    float *const sO = sS + 2 * BM + 4 + 4 * 64 * TS;  // [8][OS] X values, then [8][OS] W values
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -306,8 +309,8 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     if constexpr (kEpi == kEpiOutlier) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            sO[t * BM + tid] = oxv[t];
-            sO[(8 + t) * BM + tid] = owv[t];
+            sO[t * OS + tid] = oxv[t];
+            sO[(8 + t) * OS + tid] = owv[t];
         }
     }
     int u = 0;
@@ -364,9 +367,9 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         for (int tt = 0; tt < 2; ++tt) {
             const int t = 4 * tt + kq;
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni) ow[tt][ni] = sO[(8 + t) * BM + c0 + 16 * ni + c];
+            for (int ni = 0; ni < 8; ++ni) ow[tt][ni] = sO[(8 + t) * OS + c0 + 16 * ni + c];
 #pragma unroll
-            for (int mi = 0; mi < 8; ++mi) ox[mi][tt] = sO[t * BM + r0 + 16 * mi + c];
+            for (int mi = 0; mi < 8; ++mi) ox[mi][tt] = sO[t * OS + r0 + 16 * mi + c];
         }
     }
     typedef float v2f __attribute__((ext_vector_type(2)));
