@@ -48,10 +48,11 @@ static Variant make(const std::string &spec) {
     if (spec == "dsp") return {spec, gemm_i8_ds<kDsPacked | kDsRowMajorOrder>};
     if (spec == "dss") return {spec, gemm_i8_ds<kDsNt | kDsRowMajorOrder>};
     if (spec == "dsn") return {spec, gemm_i8_ds<kDsNt | kDsPacked>};
-    if (spec == "dsP") return {spec, gemm_i8_ds<kDsPacked | kDsPair>};
-    if (spec == "dsPn") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsPair>};
-    if (spec == "dsPT") return {spec, gemm_i8_ds<kDsPacked | kDsPair | kDsStamp>, true};
-    if (spec == "dsPnT") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsPair | kDsStamp>, true};
+    if (spec == "dsP") return {spec, gemm_i8_ds<kDsPacked | kDsPair | kDsRowMajorOrder>};
+    if (spec == "dsPn") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsPair | kDsRowMajorOrder>};
+    if (spec == "dsPnc") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsPair>};  // column bands first
+    if (spec == "dsPT") return {spec, gemm_i8_ds<kDsPacked | kDsPair | kDsRowMajorOrder | kDsStamp>, true};
+    if (spec == "dsPnT") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsPair | kDsRowMajorOrder | kDsStamp>, true};
     if (spec == "dspT") return {spec, gemm_i8_ds<kDsPacked | kDsRowMajorOrder | kDsStamp>, true};
     if (spec == "dsT") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsRowMajorOrder | kDsStamp>, true};
     if (spec == "dsX") return {spec, gemm_i8_ds<kDsPacked | kDsNoStore>, false, true};

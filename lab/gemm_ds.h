@@ -157,9 +157,11 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_ds(GemmArgs p) {
     } else if ((kFlags & kDsPair) != 0 && full) {
         const bool lo = c < 8;
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-            for (int np = 0; np < 4; ++np) {
+        for (int it = 0; it < 32; ++it) {
+                // kDsRowMajorOrder: mi outer (a 16-row group's 512 B per 4 pair stores); else np outer (one 128-B column
+                // band down the quadrant's 128 rows, then the next)
+                const int mi = (kFlags & kDsRowMajorOrder) ? it >> 2 : it & 7;
+                const int np = (kFlags & kDsRowMajorOrder) ? it & 3 : it >> 3;
                 const v4f o0 = tile_out(mi, 2 * np), o1 = tile_out(mi, 2 * np + 1);
                 v4f x1, x2;
 #pragma unroll
