@@ -195,8 +195,8 @@ constexpr int kFmThreads = 256;
 enum SplitMode { kSplitNone = 0, kSplitFirst = 2 };
 
 // kNtC: the paired full-tile output stores (rows < 64 KiB) are nontemporal -- the 64-MiB tail streams past the
-// caches (lab/ds_lab.hip: dsPn 56.30 vs plain pairs 56.99 us at 4096^3; at >= 64-KiB rows nontemporal stores ran
-// 122.6 vs 112.3 us, hence plain there)
+// caches (lab/ds_lab.hip: dsPn 56.30 vs plain pairs 56.99 us at 4096^3).  The wide-row LDS-image stores are
+// nontemporal in every instantiation (qgemm_mm_packed_i32, the one kNtC = false caller, never sets wide_rows).
 template <int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30>
 __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     static_assert(!(kI32 && kEpi != kEpiNone), "raw accumulators take no epilogue extras");
