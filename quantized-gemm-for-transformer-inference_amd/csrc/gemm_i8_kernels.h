@@ -290,11 +290,15 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi) {
+            // W first: the tile comes out C^T.  The row's two fragment loads go out before its MFMAs 2 and 6
+            // (lab/ds_lab.hip + lab/gemm_fm_var.h, profiles/r05_ds_lab.log runs 8-10, same box, interleaved: both
+            // after the row's 8 MFMAs (rounds 3-4) 57.2-57.8 us at 4096^3; after MFMAs 4 and 8 56.4, 109.4 at the
+            // 8192-row shard; before MFMAs 0 / 1 / 2 / 3 and + 4: 56.1 / 55.2 / 55.1 / 55.2, shard 106.9-107.2)
 #pragma unroll
-            for (int ni = 0; ni < 8; ++ni) mfma_agpr(acc[mi][ni], cb[ni], ca[mi]);  // W first: the tile comes out C^T
-            if (more) {
-                ld(na, nb, 2 * mi, un);
-                ld(na, nb, 2 * mi + 1, un);
+            for (int ni = 0; ni < 8; ++ni) {
+                if (more && ni == 2) ld(na, nb, 2 * mi, un);
+                if (more && ni == 6) ld(na, nb, 2 * mi + 1, un);
+                mfma_agpr(acc[mi][ni], cb[ni], ca[mi]);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
