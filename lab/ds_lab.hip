@@ -43,12 +43,15 @@ static Variant make(const std::string &spec) {
     if (spec == "fmrot") return {spec, gemm_i8_fm<>, false, false, true};  // product wide-row (LDS image) stores
     if (spec == "fo0") { Variant v{spec, gemm_i8_fm<kEpiOutlier>, false, true}; v.outlier = 0; return v; }
     if (spec == "fo8") { Variant v{spec, gemm_i8_fm<kEpiOutlier>, false, true}; v.outlier = 8; return v; }
-    // lab/gemm_fm_var.h: a row's two fragment loads before MFMA p and p + 4 of its 8
-    if (spec == "p0") return {spec, gemm_i8_fm_var<0>};
-    if (spec == "p1") return {spec, gemm_i8_fm_var<1>};
-    if (spec == "p2") return {spec, gemm_i8_fm_var<2>};
-    if (spec == "p3") return {spec, gemm_i8_fm_var<3>};
-    if (spec == "p4") return {spec, gemm_i8_fm_var<4>};
+    // lab/gemm_fm_var.h (lab/make_variant_fm.py): k0 = the product, k1 no s_setprio, k2 no sched_barrier, k3 A/B
+    // interleaved load order; pN = the row's two loads before MFMA N and N + 4
+    if (spec == "k0") return {spec, gemm_i8_fm_var<0>};
+    if (spec == "k1") return {spec, gemm_i8_fm_var<1>};
+    if (spec == "k2") return {spec, gemm_i8_fm_var<2>};
+    if (spec == "k3") return {spec, gemm_i8_fm_var<3>};
+    if (spec == "p1") return {spec, gemm_i8_fm_var<11>};
+    if (spec == "p2") return {spec, gemm_i8_fm_var<12>};
+    if (spec == "p3") return {spec, gemm_i8_fm_var<13>};
     if (spec == "r4") return {spec, gemm_i8_fm_r4<>};
     if (spec == "r4w") return {spec, gemm_i8_fm_r4<>, false, false, true};
     if (spec == "ds") return {spec, gemm_i8_ds<kDsNt | kDsPacked | kDsRowMajorOrder>};
