@@ -49,6 +49,8 @@ static Variant make(const std::string &spec) {
     if (spec == "k1") return {spec, gemm_i8_fm_var<1>};
     if (spec == "k2") return {spec, gemm_i8_fm_var<2>};
     if (spec == "k3") return {spec, gemm_i8_fm_var<3>};
+    if (spec == "g8") return {spec, gemm_i8_fm_var<4>};   // XCD patches of 8 tile-rows
+    if (spec == "g2") return {spec, gemm_i8_fm_var<5>};   // XCD patches of 2 tile-rows
     if (spec == "p1") return {spec, gemm_i8_fm_var<11>};
     if (spec == "p2") return {spec, gemm_i8_fm_var<12>};
     if (spec == "p3") return {spec, gemm_i8_fm_var<13>};
