@@ -49,6 +49,7 @@ static Variant make(const std::string &spec) {
     if (spec == "k1") return {spec, gemm_i8_fm_var<1>};
     if (spec == "k2") return {spec, gemm_i8_fm_var<2>};
     if (spec == "k3") return {spec, gemm_i8_fm_var<3>};
+    if (spec == "sw") return {spec, gemm_i8_fm_var<6>};   // rows share the first-operand (W) fragment
     if (spec == "g8") return {spec, gemm_i8_fm_var<4>};   // XCD patches of 8 tile-rows
     if (spec == "g2") return {spec, gemm_i8_fm_var<5>};   // XCD patches of 2 tile-rows
     if (spec == "p1") return {spec, gemm_i8_fm_var<11>};
