@@ -29,8 +29,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+template <int kGroupM = 4>
 __device__ __forceinline__ void group_tiles(int wgid, int tiles_m, int tiles_n, int &tm, int &tn) {
-    constexpr int kGroupM = 4;
     const int per_group = kGroupM * tiles_n;
     const int group = wgid / per_group;
     const int first_m = group * kGroupM;
@@ -221,7 +221,11 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     const int wid = xcd_remap(blockIdx.x, gridDim.x);
     const int tile = wid / S, slice = wid - tile * S;
     int tm, tn;
-    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
+    // wide output rows (FFN up): groups of 8 tile-rows -- each XCD's patch 8 x 8 tiles instead of 4 x 16 (lab/epi_lab.hip,
+    // profiles/r06_epi_lab.log: FFN-up GEMM 114.7-115.1 -> 110.2-110.6 us with the LDS-image stores, the whole call
+    // +0.9 %; the reads are not the difference: without stores FFN up and the 8192-row shard both run 93.6 us)
+    if (p.wide_rows) group_tiles<8>(tile, p.tiles_m, p.tiles_n, tm, tn);
+    else group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
     const int nsub = (int)(p.k_pad / 64);
     // this slice's sub-steps [u0, u0 + nloc) of the nsub 64-deep k-blocks (kSplitFirst: slice 0 the shorter one)
     int cut = slice * nsub / S, end = (slice + 1) * nsub / S;
