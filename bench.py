@@ -326,64 +326,34 @@ def node_phase_times(reps, warm, distributed, run_step, dev):
     return comp, gath
 
 
-def c4_node(args, qg, dev, world, rank, distributed, comm):
-    """BASELINE configs[3] as a whole-node figure: the global M = 65536 x 4096 x 4096 problem with M sharded
-    over the `world` ranks (op_mm_quantize_shard: per-rank pointer offsets into the full A and C), then the
-    in-place RCCL all-gather of C over xGMI (qgemm_allgather_rows, libqgemm_dist.so -- our own rccl.h call
-    site on `comm`, the product communicator).  Warm: 2 untimed steps, then args.node_reps steps, each
-    bracketed by a barrier; per step the max over ranks of each phase, reported as medians.  Then the
-    PIPELINED step (op_mm_quantize_shard_pipelined): W packed once, the rank's rows in chunks, chunk c's
-    broadcasts on a second stream under chunk c + 1's compute; its whole time per step, max over ranks.
-    Kept OUT of `value` (the gather moves 1 GiB of C, ~10x the compute)."""
-    import statistics
+def all_ranks_true(flag, distributed, dev):
+    """True when `flag` holds on every rank (MIN all-reduce), e.g. every rank's gathered rows matched."""
     import torch
-    Mg, N, K = 65536, 4096, 4096
-    A = qg.fill_uniform(torch.empty((Mg, K), device=dev), seed=2 * 7)  # the same A on every rank
-    B = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 7 + 1)
-    C = torch.empty((Mg, N), device=dev)
-    m0, rows = qg.shard_rows(Mg, world, rank)
-    chunks = args.node_chunks if args.node_chunks > 0 else max(1, rows // 4096)
-    hip = HipEvents(3)
-    gstream = torch.cuda.Stream(dev)
-    ws = torch.empty(qg.load_dist().op_mm_quantize_shard_pipelined_workspace_size(Mg, N, K, world, chunks),
-                     dtype=torch.uint8, device=dev)
-    probe = [qg.shard_rows(Mg, world, r)[0] for r in range(world)]
-    Cref = torch.empty((len(probe), N), device=dev)
-    for i, r0 in enumerate(probe):  # one row of every shard, by this rank's own one-GPU call
-        qg.op_mm_quantize(A[r0:r0 + 1].contiguous(), B, Cref[i:i + 1])
+    t = torch.tensor([1 if flag else 0], device=dev, dtype=torch.int32)
+    if distributed:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t[0]))
 
-    def gathered_ok():
-        torch.cuda.synchronize(dev)
-        return bool(torch.equal(C[probe].view(torch.int32), Cref.view(torch.int32)))
 
-    try:
-        def one_step():
-            torch.cuda.synchronize(dev)
-            s = qg._stream(dev)
-            hip.hip.hipEventRecord(hip.ev[0], s)
-            qg.op_mm_quantize_shard(A, B, C, world, rank)
-            hip.hip.hipEventRecord(hip.ev[1], s)
-            comm.allgather_rows(C)
-            hip.hip.hipEventRecord(hip.ev[2], s)
-            return hip.elapsed_ms(hip.ev[0], hip.ev[1]), hip.elapsed_ms(hip.ev[1], hip.ev[2])
+def c4_chunks(args, rows):
+    """Chunks per rank of the pipelined C4 step: --node-chunks, else one per 4096 rows of the rank's shard."""
+    return args.node_chunks if args.node_chunks > 0 else max(1, rows // 4096)
 
-        comp, gath = node_phase_times(args.node_reps, 2, distributed, one_step, dev)
-        serial_ok = gathered_ok()
 
-        def pipe_step():
-            torch.cuda.synchronize(dev)
-            s = qg._stream(dev)
-            hip.hip.hipEventRecord(hip.ev[0], s)
-            qg.op_mm_quantize_shard_pipelined(A, B, C, world, rank, chunks, comm=comm, gather_stream=gstream,
-                                              workspace=ws)
-            hip.hip.hipEventRecord(hip.ev[1], s)  # the call leaves s waiting for the last broadcast
-            return hip.elapsed_ms(hip.ev[0], hip.ev[1]), 0.0
-
-        C.fill_(float("nan"))
-        pipe, _ = node_phase_times(args.node_reps, 2, distributed, pipe_step, dev)
-        pipe_ok = gathered_ok()
-    finally:
-        hip.destroy()
+def c4_node_report(args, world, rows, distributed, dev, serial_step, reset, pipe_step, gathered_ok,
+                   Mg=65536, N=4096, K=4096):
+    """c4_node's host-side orchestration and its JSON: 2 warm-up + args.node_reps timed serial steps (serial_step()
+    -> this rank's (compute_ms, allgather_ms)), then the same for the pipelined step (pipe_step() -> ms) after
+    reset(); each phase's per-step MAX over ranks, reported as medians; gathered_ok() is AND-ed over the ranks after
+    each phase.  The GPU steps are bench.c4_node's; tests/test_distributed.py runs this on gloo with stub steps."""
+    import statistics
+    chunks = c4_chunks(args, rows)
+    comp, gath = node_phase_times(args.node_reps, 2, distributed, serial_step, dev)
+    serial_ok = all_ranks_true(gathered_ok(), distributed, dev)
+    reset()
+    pipe, _ = node_phase_times(args.node_reps, 2, distributed, lambda: (pipe_step(), 0.0), dev)
+    pipe_ok = all_ranks_true(gathered_ok(), distributed, dev)
     cm, gm, pm = statistics.median(comp), statistics.median(gath), statistics.median(pipe)
     return {
         "workload": f"BASELINE configs[3]: M={Mg} K=N={N} sharded over {world} GPU(s) ({Mg // world} rows each) + "
@@ -405,6 +375,59 @@ def c4_node(args, qg, dev, world, rank, distributed, comm):
         "note": "the compute is a full drop-in call per rank on its row shard (pack + GEMM); world 1: the whole "
                 "65536-row problem on one GPU and a no-op gather",
     }
+
+
+def c4_node(args, qg, dev, world, rank, distributed, comm):
+    """BASELINE configs[3] as a whole-node figure: the global M = 65536 x 4096 x 4096 problem with M sharded
+    over the `world` ranks (op_mm_quantize_shard: per-rank pointer offsets into the full A and C), then the
+    in-place RCCL all-gather of C over xGMI (qgemm_allgather_rows, libqgemm_dist.so -- our own rccl.h call
+    site on `comm`, the product communicator).  Then the PIPELINED step (op_mm_quantize_shard_pipelined): W
+    packed once, the rank's rows in chunks, chunk c's broadcasts on a second stream under chunk c + 1's compute.
+    Timing and the JSON: c4_node_report.  Kept OUT of `value` (the gather moves 1 GiB of C, ~10x the compute)."""
+    import torch
+    Mg, N, K = 65536, 4096, 4096
+    A = qg.fill_uniform(torch.empty((Mg, K), device=dev), seed=2 * 7)  # the same A on every rank
+    B = qg.fill_uniform(torch.empty((K, N), device=dev), seed=2 * 7 + 1)
+    C = torch.empty((Mg, N), device=dev)
+    m0, rows = qg.shard_rows(Mg, world, rank)
+    chunks = c4_chunks(args, rows)
+    hip = HipEvents(3)
+    gstream = torch.cuda.Stream(dev)
+    ws = torch.empty(qg.load_dist().op_mm_quantize_shard_pipelined_workspace_size(Mg, N, K, world, chunks),
+                     dtype=torch.uint8, device=dev)
+    probe = [qg.shard_rows(Mg, world, r)[0] for r in range(world)]
+    Cref = torch.empty((len(probe), N), device=dev)
+    for i, r0 in enumerate(probe):  # one row of every shard, by this rank's own one-GPU call
+        qg.op_mm_quantize(A[r0:r0 + 1].contiguous(), B, Cref[i:i + 1])
+
+    def gathered_ok():
+        torch.cuda.synchronize(dev)
+        return bool(torch.equal(C[probe].view(torch.int32), Cref.view(torch.int32)))
+
+    def serial_step():
+        torch.cuda.synchronize(dev)
+        s = qg._stream(dev)
+        hip.hip.hipEventRecord(hip.ev[0], s)
+        qg.op_mm_quantize_shard(A, B, C, world, rank)
+        hip.hip.hipEventRecord(hip.ev[1], s)
+        comm.allgather_rows(C)
+        hip.hip.hipEventRecord(hip.ev[2], s)
+        return hip.elapsed_ms(hip.ev[0], hip.ev[1]), hip.elapsed_ms(hip.ev[1], hip.ev[2])
+
+    def pipe_step():
+        torch.cuda.synchronize(dev)
+        s = qg._stream(dev)
+        hip.hip.hipEventRecord(hip.ev[0], s)
+        qg.op_mm_quantize_shard_pipelined(A, B, C, world, rank, chunks, comm=comm, gather_stream=gstream,
+                                          workspace=ws)
+        hip.hip.hipEventRecord(hip.ev[1], s)  # the call leaves s waiting for the last broadcast
+        return hip.elapsed_ms(hip.ev[0], hip.ev[1])
+
+    try:
+        return c4_node_report(args, world, rows, distributed, dev, serial_step, lambda: C.fill_(float("nan")),
+                              pipe_step, gathered_ok, Mg, N, K)
+    finally:
+        hip.destroy()
 
 
 def gemm_kernel_name(L, M, N, K, outlier):

@@ -21,8 +21,11 @@
  *   - Work is enqueued asynchronously; the plain entry point uses the null stream, like the
  *     reference's launches (legacy default stream).
  *   - No parameter is named N: the reference's op_elemwise.cuh:10 does "#define N 256".
- *   - Not re-entrant across threads on ONE device with the implicit workspace; pass an explicit
- *     workspace (op_mm_quantize_ws) for concurrent streams or for hipGraph capture.
+ *   - The entry points without a workspace argument use a grow-only device buffer cached per
+ *     (device, stream) -- per calling thread as well for hipStreamPerThread -- so calls on
+ *     different streams never share it; the reference allocates per call (op_mm.cuh:76-93).
+ *     Growing it allocates (not allowed inside a hipGraph capture) and waits for that stream;
+ *     pass an explicit workspace (op_mm_quantize_ws) for capture or to bound memory.
  */
 #ifndef QGEMM_H_
 #define QGEMM_H_

@@ -80,7 +80,10 @@ QGEMM_API size_t op_mm_quantize_shard_pipelined_workspace_size(int m, int n, int
  * packed once (qgemm_pack_b), chunk c's rows run op_mm_quantize_prepacked_ws on `stream` (bit-identical to
  * op_mm_quantize_shard), then an event hands chunk c to `gather_stream`, where the chunk's broadcasts
  * (qgemm_allgather_chunk_plan) run under chunk c + 1's compute.  On return `stream` waits for the last
- * broadcast, so work enqueued after it sees the whole C.  comm may be NULL only when world == 1 (no gather). */
+ * broadcast, so work enqueued after it sees the whole C.  comm may be NULL only when world == 1 (no gather).
+ * After a local error past the argument checks (pack, compute, event) the remaining chunks are not computed but
+ * their broadcast groups are still issued, so the peer ranks complete instead of blocking in RCCL; the first error
+ * is returned and C's rows are unspecified. */
 QGEMM_API int op_mm_quantize_shard_pipelined(const float *A, const float *B, float *C, int m, int n, int k, int world,
                                              int rank, int chunks, void *comm, void *workspace, size_t ws_bytes,
                                              void *stream, void *gather_stream);

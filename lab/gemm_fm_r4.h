@@ -67,9 +67,6 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm_r4(GemmArgs p) {
     if constexpr (kEpi == kEpiOutlier) {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) ocol[tt] = 4 * tt + (lane >> 4) < ocnt ? p.ocols[4 * tt + (lane >> 4)] : 0;
-        // the pack has read the flags accumulator: clean it for the next call (write-through, as the flags atomics are)
-        if (blockIdx.x == 0 && tid < p.ozero_words)
-            __hip_atomic_store(p.ozero + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     v4i acc[8][8];

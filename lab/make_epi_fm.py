@@ -26,7 +26,7 @@ reps = [
      '__global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {',
      'template <int kMap, int kStore, int kAux, int kEpi = kEpiNone, bool kI32 = false, int kSplit = kSplitNone, bool kNtC = !kI32, int kFirst64 = 30>\n'
      '__global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm_epi(GemmArgs p) {'),
-    ("    if (p.wide_rows) group_tiles<8>(tile, p.tiles_m, p.tiles_n, tm, tn);\n    else group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);\n",
+    ("    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn, kEpi != kEpiOutlier && p.wide_rows ? 8 : 4);\n",
      """    if constexpr (kMap == 1 || kMap == 3) {  // XCD patches of 8 (2) tile-rows instead of 4
         constexpr int kG = kMap == 1 ? 8 : 2;
         const int per_group = kG * p.tiles_n, group = tile / per_group, first_m = group * kG;
@@ -111,7 +111,7 @@ reps = [
         }
     }
     if constexpr (kStore == 2)
-        if (p.ozero_words == -12345) C[tid] = lab_sink;
+        if (p.reset_tickets == -12345) C[tid] = lab_sink;
 }"""),
 ]
 for x, y in reps:

@@ -1,13 +1,14 @@
 // api.hip -- the C-ABI of include/qgemm.h: argument checks, layout dispatch, workspace, stream order.
 //
 // op_quantized_mm (/root/reference/src/ops/op_mm.cuh:67-101) runs ten launches and allocates eight
-// temporaries per call.  Here a call is three stream-ordered launch groups on caller memory plus a
-// grow-only cached workspace:
+// temporaries per call.  Here a call is two or three stream-ordered launches on caller memory plus a
+// grow-only workspace cached per (device, stream):
 //   pack A  (Cx + X_int8)          -- op_mm.cuh:76-77, 82-83, 86-87
 //   pack B  (Cw + W_int8^T)        -- op_mm.cuh:78-79, 84-85, 88-89
 //   MFMA GEMM + dequant epilogue   -- op_mm.cuh:92-99
 #include <map>
 #include <mutex>
+#include <thread>
 #include <stdio.h>
 
 #include "../../include/qgemm.h"
@@ -34,73 +35,64 @@ hipError_t pack_vectors(const float *src, int64_t row_stride, int64_t elem_strid
     return launch_pack_rows(src, row_stride, elem_stride, rows, len, range, out, stream);
 }
 
-// Grow-only workspace per device, for the entry points without an explicit workspace.
-struct CachedWs {
+// Grow-only cached buffers for the entry points without an explicit workspace, one per (device, stream, use): a
+// buffer is only reused in its stream's order, so calls on different streams never share packed operands or split-K
+// tickets (the reference allocates its temporaries per call, op_mm.cuh:76-93).  hipStreamPerThread names a different
+// stream in every host thread, so it is keyed by the calling thread as well.  Growth waits for the owning stream only.
+enum CacheUse { kUseWorkspace = 0, kUseSplitK = 1, kUseErrorStats = 2 };  // never shared: split-K tickets stay zero
+struct CacheKey {
+    int dev;
+    hipStream_t stream;
+    std::thread::id thread;
+    int use;
+    bool operator<(const CacheKey &o) const {
+        if (dev != o.dev) return dev < o.dev;
+        if (stream != o.stream) return stream < o.stream;
+        if (thread != o.thread) return thread < o.thread;
+        return use < o.use;
+    }
+};
+struct CachedBuf {
     void *ptr = nullptr;
     size_t bytes = 0;
 };
-std::mutex g_ws_mu;
-CachedWs g_ws[64];
+std::mutex g_cache_mu;
+std::map<CacheKey, CachedBuf> g_cache;
 
-hipError_t cached_workspace(size_t need, void **out) {
+// zero_new: the buffer is zeroed when (re)allocated (split-K tickets start at zero; the launches re-zero them)
+hipError_t cached_buffer(size_t need, hipStream_t stream, int use, bool zero_new, size_t headroom, void **out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    CachedWs &w = g_ws[dev];
+    const std::thread::id th = stream == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    CachedBuf &w = g_cache[CacheKey{dev, stream, th, use}];
     if (w.bytes < need) {
         if (w.ptr) {
-            // a previous call may still be using it on some stream
-            if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+            // earlier calls on this stream may still be using it
+            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
             if ((e = hipFree(w.ptr)) != hipSuccess) return e;
             w.ptr = nullptr;
             w.bytes = 0;
         }
-        size_t grow = need + need / 8;  // headroom for nearby shapes
+        const size_t grow = need + headroom;
         if ((e = hipMalloc(&w.ptr, grow)) != hipSuccess) return e;
+        if (zero_new && (e = hipMemset(w.ptr, 0, grow)) != hipSuccess) return e;
         w.bytes = grow;
     }
     *out = w.ptr;
     return hipSuccess;
 }
 
+hipError_t cached_workspace(size_t need, hipStream_t stream, void **out) {
+    return cached_buffer(need, stream, kUseWorkspace, false, need / 8 /* headroom for nearby shapes */, out);
+}
+
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Split-K scratch for qgemm_mm_packed (which has no workspace argument): grow-only, one per
-// (device, stream) -- the tickets and slabs are only safe to reuse in stream order.
-enum ScratchUse { kScratchSplitK = 0, kScratchErrorStats = 1 };  // never shared: split-K tickets must stay zero
-struct ScratchKey {
-    int dev;
-    hipStream_t stream;
-    int use;
-    bool operator<(const ScratchKey &o) const {
-        if (dev != o.dev) return dev < o.dev;
-        if (stream != o.stream) return stream < o.stream;
-        return use < o.use;
-    }
-};
-std::mutex g_scratch_mu;
-std::map<ScratchKey, CachedWs> g_scratch;
+// Split-K scratch of qgemm_mm_packed and the error-statistics scratch (no workspace argument): zeroed at allocation.
 hipError_t cached_scratch(size_t need, hipStream_t stream, int use, void **out) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    std::lock_guard<std::mutex> lk(g_scratch_mu);
-    CachedWs &w = g_scratch[ScratchKey{dev, stream, use}];
-    if (w.bytes < need) {
-        if (w.ptr) {
-            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
-            if ((e = hipFree(w.ptr)) != hipSuccess) return e;
-            w.ptr = nullptr;
-            w.bytes = 0;
-        }
-        if ((e = hipMalloc(&w.ptr, need)) != hipSuccess) return e;
-        if ((e = hipMemset(w.ptr, 0, need)) != hipSuccess) return e;  // split-K tickets start at zero
-        w.bytes = need;
-    }
-    *out = w.ptr;
-    return hipSuccess;
+    return cached_buffer(need, stream, use, true, 0, out);
 }
 
 hipError_t mm_packed_impl(const void *packed_a, const void *packed_b, float *C, int64_t c_stride_h,
@@ -152,7 +144,7 @@ int qgemm_mm_packed(const void *packed_a, const void *packed_b, float *C, int64_
     void *scratch = nullptr;
     const size_t sb = gemm_scratch_bytes(m, n, k);
     if (sb) {
-        hipError_t e = cached_scratch(sb, s, kScratchSplitK, &scratch);
+        hipError_t e = cached_scratch(sb, s, kUseSplitK, &scratch);
         if (e != hipSuccess) return err(e);
     }
     return err(mm_packed_impl(packed_a, packed_b, C, c_stride_h, c_stride_w, m, n, k, range, scratch, sb, s,
@@ -212,7 +204,7 @@ int op_mm_quantize_ex(const float *A, int64_t a_stride_h, int64_t a_stride_w, co
     if (m == 0 || n == 0) return 0;
     const size_t need = op_mm_quantize_workspace_size(m, n, k);
     void *ws = nullptr;
-    hipError_t e = cached_workspace(need, &ws);
+    hipError_t e = cached_workspace(need, static_cast<hipStream_t>(stream), &ws);
     if (e != hipSuccess) return err(e);
     return op_mm_quantize_ws(A, a_stride_h, a_stride_w, B, b_stride_h, b_stride_w, C, c_stride_h, c_stride_w, m, n, k,
                              range, ws, need, stream);
@@ -236,7 +228,7 @@ int qgemm_error_stats(const float *C, const float *O, int64_t count, int referen
     if (!C || !O || !stats || count < 1) return err(hipErrorInvalidValue);
     hipStream_t s = static_cast<hipStream_t>(stream);
     void *scratch = nullptr;
-    hipError_t e = cached_scratch(error_stats_scratch_bytes(), s, kScratchErrorStats, &scratch);
+    hipError_t e = cached_scratch(error_stats_scratch_bytes(), s, kUseErrorStats, &scratch);
     if (e != hipSuccess) return err(e);
     return err(launch_error_stats(C, O, count, reference_order != 0, stats, scratch, s));
 }
@@ -278,7 +270,7 @@ int op_mm_quantize_prepacked(const float *A, const void *packed_b, float *C, int
     if (m == 0 || n == 0) return 0;
     const size_t need = qgemm_linear_workspace_size(m, n, k);
     void *ws = nullptr;
-    hipError_t e = cached_workspace(need, &ws);
+    hipError_t e = cached_workspace(need, nullptr, &ws);
     if (e != hipSuccess) return err(e);
     return op_mm_quantize_prepacked_ws(A, k, packed_b, C, n, m, n, k, ws, need, nullptr);
 }

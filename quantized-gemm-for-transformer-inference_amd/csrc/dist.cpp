@@ -167,39 +167,40 @@ int op_mm_quantize_shard_pipelined(const float *A, const float *B, float *C, int
     char *ws = static_cast<char *>(workspace);
     // W packed ONCE for every chunk (the prepacked drop-in is bit-identical to op_mm_quantize)
     int rc = qgemm_pack_b(B, n, 1, k, n, 127.0f, ws, s);
-    if (rc) return rc;
     hipEvent_t ev = nullptr;
     hipError_t he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (he != hipSuccess) return (int)he;
+    if (he != hipSuccess && rc == 0) rc = (int)he;
+    // After a local error (pack, compute, event) the remaining chunks are not computed, but their broadcast groups
+    // are still issued, in plan order: the peer ranks issue theirs and would otherwise block in RCCL for ever.  The
+    // first error is returned and the rows of C are then unspecified.
     int op = 0;
-    for (int c = 0; c < chunks && rc == 0; ++c) {
+    for (int c = 0; c < chunks; ++c) {
         int c0 = 0, crows = 0;
         qgemm_shard_rows(rows, chunks, c, &c0, &crows);
-        if (crows > 0)
+        if (crows > 0 && rc == 0)
             rc = op_mm_quantize_prepacked_ws(A + (int64_t)(m0 + c0) * k, k, ws, C + (int64_t)(m0 + c0) * n, n, crows,
                                              n, k, ws + pb_bytes, ws_bytes - pb_bytes, s);
         // this chunk's broadcasts (every owner's chunk c) on the gather stream, behind this rank's compute of it;
         // the event is re-recorded per chunk: hipStreamWaitEvent captures the record it follows
         const int o0 = op;
         while (op < nops && chunk_of[(size_t)op] == c) ++op;
-        if (rc || !cm || op == o0) continue;
-        if ((he = hipEventRecord(ev, s)) != hipSuccess || (he = hipStreamWaitEvent(g, ev, 0)) != hipSuccess) {
+        if (!cm || op == o0) continue;
+        if (rc == 0 &&
+            ((he = hipEventRecord(ev, s)) != hipSuccess || (he = hipStreamWaitEvent(g, ev, 0)) != hipSuccess))
             rc = (int)he;
-            break;
-        }
         ncclResult_t r = ncclGroupStart();
         for (int i = o0; i < op && r == ncclSuccess; ++i)
             r = ncclBroadcast(C + first[(size_t)i], C + first[(size_t)i], (size_t)count[(size_t)i], ncclFloat32,
                               root[(size_t)i], cm, g);
         const ncclResult_t r2 = ncclGroupEnd();
-        rc = nccl_rc(r != ncclSuccess ? r : r2);
+        if (rc == 0) rc = nccl_rc(r != ncclSuccess ? r : r2);
     }
     // the caller's stream sees the whole C: it waits for the last broadcast
     if (rc == 0 && cm && op > 0) {
         if ((he = hipEventRecord(ev, g)) != hipSuccess || (he = hipStreamWaitEvent(s, ev, 0)) != hipSuccess)
             rc = (int)he;
     }
-    (void)hipEventDestroy(ev);  // released once its last record completes
+    if (ev) (void)hipEventDestroy(ev);  // released once its last record completes
     return rc;
 }
 

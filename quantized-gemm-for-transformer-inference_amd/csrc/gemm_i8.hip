@@ -217,8 +217,7 @@ bool gemm_outlier_ok(int m, int n, int k) {
 
 hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b, float *C, int64_t csh, int m, int n,
                                        float inv_r2, const float *x, int64_t xsh, const float *w, int64_t wsh,
-                                       const int *ocols, const int *ocount, uint32_t *ozero, int ozero_words,
-                                       hipStream_t stream) {
+                                       const int *ocols, const int *ocount, hipStream_t stream) {
     if (!shape_ok(a, b) || !gemm_outlier_ok(m, n, (int)a.k_pad)) return hipErrorNotSupported;
     const GemmPlan g = gemm_plan(m, n, (int)a.k_pad);
     GemmArgs p{a.q, b.q, a.scale, b.scale, C, csh, 1, m, n, a.k_pad, g.tiles_m, g.tiles_n,
@@ -226,8 +225,6 @@ hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b,
     p.wide_rows = csh >= 16384 ? 1 : 0;
     p.xo_ld = xsh;
     p.ocols = ocols;
-    p.ozero = ozero;
-    p.ozero_words = ozero_words;
     return launch_v3<kEpiOutlier>(p, dim3((unsigned)(g.tiles_m * g.tiles_n)), stream);
 }
 

@@ -29,8 +29,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int kGroupM = 4>
-__device__ __forceinline__ void group_tiles(int wgid, int tiles_m, int tiles_n, int &tm, int &tn) {
+__device__ __forceinline__ void group_tiles(int wgid, int tiles_m, int tiles_n, int &tm, int &tn, int kGroupM = 4) {
     const int per_group = kGroupM * tiles_n;
     const int group = wgid / per_group;
     const int first_m = group * kGroupM;
@@ -74,8 +73,6 @@ struct GemmArgs {
     int wide_rows;
     int64_t xo_ld;
     const int *ocols;
-    uint32_t *ozero;  // kEpiOutlier: workgroup 0 zeroes ozero[0 .. ozero_words) (the consumed flags accumulator)
-    int ozero_words;
 };
 
 // Epilogue extras for the encoder's linears (linear.cuh:52-54 then op_relu, transformer.cu:66):
@@ -223,9 +220,10 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
     int tm, tn;
     // wide output rows (FFN up): groups of 8 tile-rows -- each XCD's patch 8 x 8 tiles instead of 4 x 16 (lab/epi_lab.hip,
     // profiles/r06_epi_lab.log: FFN-up GEMM 114.7-115.1 -> 110.2-110.6 us with the LDS-image stores, the whole call
-    // +0.9 %; the reads are not the difference: without stores FFN up and the 8192-row shard both run 93.6 us)
-    if (p.wide_rows) group_tiles<8>(tile, p.tiles_m, p.tiles_n, tm, tn);
-    else group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn);
+    // +0.9 %; the reads are not the difference: without stores FFN up and the 8192-row shard both run 93.6 us).  Not
+    // in the outlier epilogue's instantiation: there the runtime group size made hipcc move its accumulators (+186
+    // v_accvgpr_mov, c2_outlier's GEMM 58.9 -> 61.8 us, same box)
+    group_tiles(tile, p.tiles_m, p.tiles_n, tm, tn, kEpi != kEpiOutlier && p.wide_rows ? 8 : 4);
     const int nsub = (int)(p.k_pad / 64);
     // this slice's sub-steps [u0, u0 + nloc) of the nsub 64-deep k-blocks (kSplitFirst: slice 0 the shorter one)
     int cut = slice * nsub / S, end = (slice + 1) * nsub / S;
@@ -268,9 +266,6 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
             oxv[t] = t < ocnt && i < p.m ? p.xo[i * p.xo_ld + col] : 0.0f;
             owv[t] = t < ocnt ? (j < p.n ? p.wo[(int64_t)col * p.wo_ld + j] : 0.0f) : -0.0f;
         }
-        // the pack has read the flags accumulator: clean it for the next call (write-through, as the flags atomics are)
-        if (blockIdx.x == 0 && tid < p.ozero_words)
-            __hip_atomic_store(p.ozero + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     v4i acc[8][8];

@@ -127,21 +127,38 @@ __device__ __forceinline__ void zero_words_block0(uint32_t *words, int n) {
 // column when bit k of `bits` is set.  The int8 chain runs on X' / W' = X / W with those columns /
 // rows zeroed, so the packs treat them as +0 (absmax candidates, the signed seed and the quantized
 // bytes alike, exactly as packing the zeroed copies).  The fp32 part reads the original values from X and W
-// themselves (gemm_i8_fm<kEpiOutlier>), so nothing is written here but the column index.  The mask is the flags
-// launch's accumulator (outlier.hip: nwords <= 128 words, bit c of word w = column 32 w + c), read by every
-// thread for exactly the words of its own elements, issued ahead of its data: an X-row lane's chunk l + 64 j
+// themselves (gemm_i8_fm<kEpiOutlier>), so nothing is written here but the column index.  The mask comes from the
+// flags launch as nparts partial masks (outlier.hip outlier_colmask_kernel: partial[p][w] for row split p, every word
+// written by it each call, so no state lives on between calls; nparts = 2 at K = 4096): word w = OR over p.  Each
+// thread reads exactly the words of its own elements, issued ahead of its data: an X-row lane's chunk l + 64 j
 // (columns 4 (l + 64 j) .. +3) is nibble l & 7 of word (l >> 3) + 8 j, a W-strip thread's rows 4 q + e + 1024 i
 // are bits of word (4 q + 1024 i) >> 5.  Workgroup 0 also builds the column count and the ascending list for the
 // GEMM (idx[0], idx[1 ..]).
 struct OutlierMask {
-    const uint32_t *acc;  // nwords mask words (bit 0 of word 0: column 0, the absmax seed)
-    int nwords;
-    int *idx;             // out: [count][columns ascending]
+    const uint32_t *partial;  // nparts x nwords partial mask words (bit 0 of word 0: column 0, the absmax seed)
+    int nwords, nparts;
+    int *idx;                 // out: [count][columns ascending]
+    // mask words w[j] (0 where w[j] >= nwords): the ORs of their nparts partial words -- every load of split 0 issued
+    // before any is waited for (nparts is 1 or 2 on the shapes the benchmarks run)
+    template <int NW>
+    __device__ __forceinline__ void words(const int (&w)[NW], uint32_t (&out)[NW]) const {
+#pragma unroll
+        for (int j = 0; j < NW; ++j) out[j] = w[j] < nwords ? partial[w[j]] : 0u;
+        for (int p = 1; p < nparts; ++p)
+#pragma unroll
+            for (int j = 0; j < NW; ++j) out[j] |= w[j] < nwords ? partial[p * nwords + w[j]] : 0u;
+    }
+    __device__ __forceinline__ uint32_t word(int w) const {
+        const int ws[1] = {w};
+        uint32_t x[1];
+        words(ws, x);
+        return x[0];
+    }
 };
 // workgroup 0 of the masked pack: idx[0] = the outlier columns, idx[1 ..] = them ascending (nwords <= blockDim)
 __device__ __forceinline__ void outlier_column_list(const OutlierMask &om, int *wsum /* LDS, blockDim / 64 */) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nwave = blockDim.x >> 6;
-    const uint32_t word = t < om.nwords ? om.acc[t] : 0u;
+    const uint32_t word = t < om.nwords ? om.word(t) : 0u;
     const int pc = __popc(word);
     int x = pc;
 #pragma unroll
@@ -198,26 +215,27 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         // buffer loads on one per-lane offset; chunks >= nfull lie past the descriptor and read as zeros
         typedef int v4i_t __attribute__((ext_vector_type(4)));
         const auto rs = buf_rsrc(srow, (uint32_t)nfull * 16);
-        // the lane's mask words (chunk lane + 64 j: word (lane >> 3) + 8 j), issued ahead of the row so that they
-        // arrive with it
-        uint32_t mwd[R > 0 ? R : 1];
-        if constexpr (kMask) {
-            static_assert(R <= 16, "the mask words cover len <= 4096");
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const int w = (lane >> 3) + 8 * j;
-                mwd[j] = w < om->nwords ? om->acc[w] : 0u;
-            }
-        }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(lane + j * kWave) * 16, 0, 0);
             v[j] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
+        // the lane's mask words (chunk lane + 64 j: word (lane >> 3) + 8 j), issued behind the row's loads so that
+        // both latencies overlap (a row split past the first ORs behind a wait)
+        uint32_t mwd[R > 0 ? R : 1];
+        uint32_t mw0 = 0u;  // word 0: its bit 0 masks the absmax seed
+        if constexpr (kMask) {
+            static_assert(R <= 16, "the mask words cover len <= 4096");
+            int wj[R > 0 ? R : 1];
+#pragma unroll
+            for (int j = 0; j < R; ++j) wj[j] = (lane >> 3) + 8 * j;
+            om->words(wj, mwd);
+            mw0 = om->word(0);
+        }
         if constexpr (kMask) {
             // outlier columns: X' holds +0 there (the seed included); branch-free selects
             {
-                if (om->acc[0] & 1u) seed = 0.0f;
+                if (mw0 & 1u) seed = 0.0f;
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     const uint32_t nib = (mwd[j] >> (4 * (lane & 7))) & 15u;
@@ -1003,15 +1021,6 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     const float w_seed = t < kWs8Cols ? w[n0 + t] : 0.0f;  // W[0, j], issued first (used after the reduction)
     const auto src = buf_rsrc(w + n0, (uint32_t)(((int64_t)(k - 1) * wsh + kWs8Cols) * 4));
     const uint32_t vrow = (uint32_t)((4 * rq * wsh + 4 * c2) * 4);
-    // the mask words of the thread's rows (4 rq + e + 1024 i: word (4 rq + 1024 i) >> 5), issued ahead of the strip's
-    // loads
-    uint32_t mw[4] = {0u, 0u, 0u, 0u};
-    if constexpr (kMask)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = (4 * rq + 1024 * i) >> 5;
-            mw[i] = w < om->nwords ? om->acc[w] : 0u;
-        }
     float4 v[4][4];  // [i][e]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1020,11 +1029,21 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
             const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(src, vrow + (uint32_t)((e + 1024 * i) * wsh * 4), 0, 0);
             v[i][e] = make_float4(__int_as_float(x[0]), __int_as_float(x[1]), __int_as_float(x[2]), __int_as_float(x[3]));
         }
+    // the mask words of the thread's rows (4 rq + e + 1024 i: word (4 rq + 1024 i) >> 5), issued behind the strip's
+    // loads
+    uint32_t mw[4] = {0u, 0u, 0u, 0u}, mw0 = 0u;  // mw0: word 0, whose bit 0 masks the absmax seed
+    if constexpr (kMask) {
+        int wi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wi[i] = (4 * rq + 1024 * i) >> 5;
+        om->words(wi, mw);
+        mw0 = om->word(0);
+    }
     bool seed_masked = false;
     if constexpr (kMask) {
         // outlier rows of W (outlier feature columns of X): W' holds +0 there; branch-free selects
         {
-            seed_masked = om->acc[0] & 1u;
+            seed_masked = mw0 & 1u;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1313,14 +1332,14 @@ bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, cons
 }
 
 hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *acc,
-                                           int nwords, int *idx, hipStream_t stream) {
+                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *partial,
+                                           int nparts, int nwords, int *idx, hipStream_t stream) {
     if (!pack_single_pass_outlier_ok(x, xsh, m, k, w, wsh, n)) return hipErrorNotSupported;
     const int nstrips = n / kWs8Cols;
     const int npad = (int)((outw.rows_pad - n) / kWs8Cols);
     const int nx = (int)(outx.rows_pad / 8);
-    if (nwords > 128) return hipErrorNotSupported;  // K <= 4096, the single pass's envelope
-    const OutlierMask om{acc, nwords, idx};
+    if (nwords > 128 || nparts < 1 || nparts > 16) return hipErrorNotSupported;  // K <= 4096: the single pass's envelope
+    const OutlierMask om{partial, nwords, nparts, idx};
     // a 4-waves-per-SIMD register budget (102 VGPRs, the same two blocks per CU): at 5 the masked body spilled
     // 20 B per lane (profiles/r03_ab_maskpack_wpe.log)
     pack_single_pass8_kernel<4, true><<<nstrips + npad + nx, 512, 0, stream>>>(

@@ -141,13 +141,14 @@ hipError_t launch_pack_single_pass_kind(const float *x, int64_t xsh, int m, int 
                                         int64_t wsh, int n, PackedView outw, float range, hipStream_t stream, int kind,
                                         uint32_t *zero_words = nullptr, int nzero = 0);
 // The single-pass pack (8-column W strips) of the LLM.int8() decomposition's int8 part: outlier columns
-// of X / rows of W packed as +0 (acc: the flags launch's nwords mask words, bit c of word w = column 32 w + c);
-// workgroup 0 writes idx[0] = the outlier count, idx[1 ..] = the columns ascending.  hipErrorNotSupported outside
-// the single pass's envelope (K % 4 == 0 too).
+// of X / rows of W packed as +0 (the mask = OR of the flags launch's nparts x nwords partial words partial[p][w],
+// bit c of word w = column 32 w + c); workgroup 0 writes idx[0] = the outlier count, idx[1 ..] = the columns
+// ascending.  hipErrorNotSupported outside the single pass's envelope (K % 4 == 0 too) or for nparts > 16 (nothing
+// launched).
 bool pack_single_pass_outlier_ok(const float *x, int64_t xsh, int m, int k, const float *w, int64_t wsh, int n);
 hipError_t launch_pack_single_pass_outlier(const float *x, int64_t xsh, int m, int k, PackedView outx, const float *w,
-                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *acc,
-                                           int nwords, int *idx, hipStream_t stream);
+                                           int64_t wsh, int n, PackedView outw, float range, const uint32_t *partial,
+                                           int nparts, int nwords, int *idx, hipStream_t stream);
 hipError_t launch_pack_cols_pass2(const float *src, int64_t sh, int len, int cols, float range, PackedView out,
                                   hipStream_t stream);
 hipError_t launch_fill_uniform(float *dst, int64_t count, uint64_t seed, float lo, float hi, hipStream_t stream);
@@ -168,14 +169,11 @@ hipError_t launch_gemm_dequant(const PackedView &a, const PackedView &b, float *
                                const float *bias = nullptr, bool relu = false, bool tickets_zeroed = false);
 // The LLM.int8() decomposition's GEMM: int8 part + the outlier columns' fp32 products in the epilogue, read from
 // X (m x k, row stride xsh) and W (k x n, row stride wsh) at the columns / rows ocols[0 .. *ocount) (ascending).
-// Workgroup 0 zeroes ozero[0 .. ozero_words) (the flags accumulator the pack has consumed) for the next call.
-// Only where the plan is the
-// 256-tile GEMM without split-K (gemm_outlier_ok); hipErrorNotSupported otherwise.
+// Only where the plan is the 256-tile GEMM without split-K (gemm_outlier_ok); hipErrorNotSupported otherwise.
 bool gemm_outlier_ok(int m, int n, int k);
 hipError_t launch_gemm_dequant_outlier(const PackedView &a, const PackedView &b, float *C, int64_t csh, int m, int n,
                                        float inv_r2, const float *x, int64_t xsh, const float *w, int64_t wsh,
-                                       const int *ocols, const int *ocount, uint32_t *ozero, int ozero_words,
-                                       hipStream_t stream);
+                                       const int *ocols, const int *ocount, hipStream_t stream);
 hipError_t launch_gemm_i32(const PackedView &a, const PackedView &b, int32_t *Acc, int m, int n,
                            hipStream_t stream);
 hipError_t launch_mm_f32(const float *A, int64_t ash, int64_t asw, const float *B, int64_t bsh, int64_t bsw, float *C,

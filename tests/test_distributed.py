@@ -6,7 +6,8 @@ product's own pieces:
   ncclAllGather / ncclBroadcast calls qgemm_allgather_rows enqueues, with the same in-place offsets) on
   gloo collectives over CPU tensors;
 * bench.py's c4_node orchestration (share_comm_id: the communicator id over broadcast_object_list;
-  node_phase_times: the per-step barrier + MAX all-reduce) runs on gloo with a stub step.
+  node_phase_times: the per-step barrier + MAX all-reduce; c4_node_report: the whole C4 report a SCALE line
+  carries, serial and pipelined phases) runs on gloo with stub compute, gather and pipeline steps.
 
 Each rank's rows are computed by the CPU oracle here (no GPU in this container); the GPU side of the same
 partition is tests/test_gpu_dist.py.  Cx is per row and Cw depends only on W, so the sharded result must
@@ -89,3 +90,79 @@ def test_msharded_gather_matches_single_process(oracle, tmp_path, M):
         assert uid.tobytes() == bytes(range(7, 7 + 128)), f"rank {r} comm id"
         # steps 2..5 after 2 warm-ups; rank-wise MAX: (1+r, 5-r) -> (2, 5); (2(r+1), 1) -> (4, 1); (0.5, 0.25+r) -> (0.5, 1.25)
         assert list(times) == [0.5, 2.0, 4.0, 0.5, 1.25, 5.0, 1.0, 1.25], f"rank {r} phase maxima"
+
+
+def _report_worker(rank, world, port, out_dir):
+    import json
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    sys.path.insert(0, os.path.join(repo, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import _pkg
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    qg = _pkg.package()
+    args = bench.parse(["--gpus", str(world), "--node-reps", "5"])
+    m0, rows = qg.shard_rows(65536, world, rank)  # the product's partition (libqgemm_dist.so)
+    # stub steps: this rank's (compute, gather) ms per step and pipelined ms; rank 1 is slower in compute, rank 0
+    # in the gather, so the per-step MAX over ranks picks from both
+    serial = iter([(0.15 + 0.01 * rank, 0.9 - 0.05 * rank + 0.001 * i) for i in range(7)])
+    pipe = iter([0.95 + 0.02 * rank + 0.001 * i for i in range(7)])
+    ok = iter([True, rank == 0])  # serial rows match everywhere; the pipelined phase fails on rank 1
+    resets = []
+    rep = bench.c4_node_report(args, world, rows, True, torch.device("cpu"), lambda: next(serial),
+                               lambda: resets.append(1), lambda: next(pipe), lambda: next(ok))
+    with open(os.path.join(out_dir, f"report{rank}.json"), "w") as f:
+        json.dump({"report": rep, "resets": len(resets), "rows": rows}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_c4_node_report_world2_on_gloo(tmp_path):
+    """bench.c4_node's orchestration at world 2 with stub compute / gather / pipeline steps --
+    the fields a SCALE line's c4_node carries: per-step MAX over ranks then medians, the all-gather GB/s received per
+    rank, chunks_per_rank == rows // 4096, and the gathered-rows checks AND-ed over the ranks."""
+    import json
+    world = 2
+    mp.spawn(_report_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    reps = [json.load(open(tmp_path / f"report{r}.json")) for r in range(world)]
+    for r, got in enumerate(reps):
+        rep = got["report"]
+        assert got["rows"] == 32768 and got["resets"] == 1
+        assert rep["world"] == 2 and rep["shard_rows"] == 32768 and rep["global_M"] == 65536 and rep["reps"] == 5
+        # timed steps i = 2..6: compute max = 0.16, gather max = 0.9 + 0.001 i (rank 0) -> median i = 4: 0.904
+        assert rep["compute_ms_median"] == 0.16 and rep["allgather_ms_median"] == 0.904, rep
+        assert rep["allgather_GBps_recv_per_rank"] == round(65536 * 4096 * 4 * 0.5 / 0.904e-3 / 1e9, 1)
+        assert rep["node_gemms_per_s_compute"] == round(1e3 / 0.16, 2)
+        assert rep["node_gemms_per_s_with_allgather"] == round(1e3 / (0.16 + 0.904), 2)
+        pipe = rep["pipelined"]
+        assert pipe["chunks_per_rank"] == 32768 // 4096 == 8
+        assert pipe["ms_median"] == round(0.97 + 0.004, 4)  # rank 1's 0.97 + 0.001 i, median i = 4
+        assert rep["gathered_rows_match_one_gpu"] is True
+        assert pipe["gathered_rows_match_one_gpu"] is False, "rank 1's failed check must reach every rank"
+
+
+def test_c4_node_report_world8_shapes():
+    """The world-8 branch of c4_node's report, one process: 8192-row shards, 2 chunks per rank (the N = 8 SCALE
+    line stays unmeasured on hardware: no 8-GPU node in any round)."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import _pkg
+    qg = _pkg.package()
+    args = bench.parse(["--node-reps", "3"])
+    for rank in (0, 7):
+        m0, rows = qg.shard_rows(65536, 8, rank)
+        assert (m0, rows) == (8192 * rank, 8192)
+        it = iter([(0.1, 0.9)] * 5)
+        rep = bench.c4_node_report(args, 8, rows, False, torch.device("cpu"), lambda: next(it), lambda: None,
+                                   lambda: 1.0, lambda: True)
+        assert rep["pipelined"]["chunks_per_rank"] == 2 and rep["shard_rows"] == 8192
+        assert rep["allgather_GBps_recv_per_rank"] == round(65536 * 4096 * 4 * 7 / 8 / 0.9e-3 / 1e9, 1)

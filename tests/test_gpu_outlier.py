@@ -133,10 +133,10 @@ def test_decomposition_reduces_quantization_error(qg, oracle, device):
 
 def test_outlier_graph_capture_and_repeat(qg, oracle, device):
     """qgemm_mm_outlier makes no allocation and no host sync (the outlier count stays on the device; the flags
-    launch's arrival ticket is a zero-initialised slot of the code object), so the three fast-path launches
-    (flags with the last-arriver index, masked pack, GEMM with the chain) can be captured in a HIP graph --
-    here as the FIRST call on its stream -- and replayed; and 20 eager calls on one workspace give the same
-    bits every time (race screen of the partial-mask / last-arriver / rank / compact-value hand-offs)."""
+    launch's counters and accumulator live in the workspace and a kernel zeroes them at the start of every call), so
+    the four fast-path launches (zero state, flags, masked pack, GEMM with the chain) can be captured in a HIP graph
+    -- here as the FIRST call on its stream -- and replayed; and 20 eager calls on one workspace give the same bits
+    every time (race screen of the accumulator / count / column-list hand-offs)."""
     import torch
     M, N, K = 2560, 4096, 512
     X, W = _with_outliers(oracle, M, N, K, [0, 5, 77, 300, 511], 12)
@@ -209,8 +209,8 @@ def test_outlier_fast_path_at_the_benched_shape(qg, oracle, device, ncols):
 
 
 def test_outlier_unaligned_workspace_bit_exact(qg, oracle, device):
-    """A caller workspace that is only 4-B aligned: the fast path keeps nothing wider than an int in it (the count
-    and column list; the mask words live in the library's per-stream accumulator), so it runs there, bit-exact."""
+    """A caller workspace that is only 4-B aligned: the fast path keeps nothing wider than an int in it (the count,
+    the column list, the flags counters and mask words), so it runs there, bit-exact."""
     M, N, K = 2560, 4096, 256
     X, W = _with_outliers(oracle, M, N, K, [1, 100, 255], 14)
     want, wcnt = oracle.mm_outlier(X, W, 6.0)
@@ -225,3 +225,77 @@ def test_outlier_unaligned_workspace_bit_exact(qg, oracle, device):
     torch.cuda.synchronize()
     assert wcnt == 3
     assert_bits_equal(O.cpu().numpy(), want, "outlier, 4-B aligned workspace")
+
+
+def _outlier_call(L, Xd, Wd, O, M, N, K, ws, stream):
+    return L.qgemm_mm_outlier(Xd.data_ptr(), Wd.data_ptr(), O.data_ptr(), M, N, K, 6.0, ws.data_ptr(), ws.numel(),
+                              stream)
+
+
+def _outlier_case(qg, oracle, device, M, N, K, cols, seed):
+    L = qg.load()
+    X, W = _with_outliers(oracle, M, N, K, cols, seed)
+    want, wcnt = oracle.mm_outlier(X, W, 6.0)
+    assert wcnt == len(cols)
+    return (_dev(X, device), _dev(W, device), want,
+            torch.empty(L.qgemm_mm_outlier_workspace_size(M, N, K), dtype=torch.uint8, device=device),
+            torch.full((M, N), float("nan"), device=device), torch.cuda.Stream(device))
+
+
+@pytest.mark.parametrize("M,N,K", [(2560, 4096, 512), (300, 200, 516)])  # fast path; materialising fallback
+def test_outlier_concurrent_streams_bit_exact(qg, oracle, device, M, N, K):
+    """the flags launch's state (counters, mask accumulator) belongs to the call, in its workspace -- not
+    to a library slot keyed by the stream handle.  Two streams run outlier calls at the same time, each with its own
+    workspace and its own outlier columns; every output bit-exact."""
+    L = qg.load()
+    cases = [_outlier_case(qg, oracle, device, M, N, K, cols, 21 + i)
+             for i, cols in enumerate(([0, 5, 77], [3, 300, 511, 64]))]
+    torch.cuda.synchronize()
+    for _ in range(8):
+        for Xd, Wd, _, ws, O, s in cases:
+            assert _outlier_call(L, Xd, Wd, O, M, N, K, ws, s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    for i, (_, _, want, _, O, _) in enumerate(cases):
+        assert_bits_equal(O.cpu().numpy(), want, f"outlier stream {i}, {M}x{N}x{K}")
+
+
+def test_outlier_graph_replay_beside_eager_calls(qg, oracle, device):
+    """a graph captured from qgemm_mm_outlier replayed while eager outlier calls (other inputs, other
+    workspace) run on another stream, and on the capture stream between replays: nothing is shared between them."""
+    L = qg.load()
+    M, N, K = 2560, 4096, 512
+    XA, WA, wantA, wsA, OA, sA = _outlier_case(qg, oracle, device, M, N, K, [0, 5, 77], 31)
+    XB, WB, wantB, wsB, OB, sB = _outlier_case(qg, oracle, device, M, N, K, [3, 300, 511, 64], 32)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sA):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=sA):
+            assert _outlier_call(L, XA, WA, OA, M, N, K, wsA, sA.cuda_stream) == 0
+    for _ in range(4):
+        with torch.cuda.stream(sA):
+            g.replay()
+        assert _outlier_call(L, XB, WB, OB, M, N, K, wsB, sB.cuda_stream) == 0
+        assert _outlier_call(L, XB, WB, OB, M, N, K, wsB, sA.cuda_stream) == 0  # eager on the capture stream
+    torch.cuda.synchronize()
+    assert_bits_equal(OA.cpu().numpy(), wantA, "graph replay beside eager calls")
+    assert_bits_equal(OB.cpu().numpy(), wantB, "eager calls beside graph replays")
+
+
+def test_outlier_on_more_than_256_streams(qg, oracle, device):
+    """round 5 gave each stream handle one of 256 library slots, never returned, so a process that had
+    used 256 streams got hipErrorOutOfMemory from every later outlier call.  300 new streams, one call each (fast
+    path and fallback shapes alternating), every result compared on the device."""
+    L = qg.load()
+    shapes = [(2560, 4096, 128, [1, 64]), (64, 96, 130, [0, 129])]
+    cases = []
+    for M, N, K, cols in shapes:
+        Xd, Wd, want, ws, O, _ = _outlier_case(qg, oracle, device, M, N, K, cols, 41)
+        cases.append((M, N, K, Xd, Wd, torch.from_numpy(want).to(device), ws, O))
+    for i in range(300):
+        M, N, K, Xd, Wd, want, ws, O = cases[i % 2]
+        s = torch.cuda.Stream(device)
+        O.fill_(float("nan"))
+        torch.cuda.synchronize()
+        assert _outlier_call(L, Xd, Wd, O, M, N, K, ws, s.cuda_stream) == 0, f"stream {i}"
+        s.synchronize()
+        assert torch.equal(O.view(torch.int32), want.view(torch.int32)), f"stream {i}, {M}x{N}x{K}"

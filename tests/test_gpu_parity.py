@@ -528,6 +528,33 @@ def test_concurrent_streams_with_own_workspaces(qg, oracle, device):
         assert_bits_equal(O.cpu().numpy(), want, f"stream {i}")
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 1024, 1024), (512, 1024, 4096)])  # plain plan; split-K plan
+def test_implicit_workspace_two_streams(qg, oracle, device, M, N, K):
+    """op_mm_quantize_ex WITHOUT a workspace, on two streams back to back with different inputs
+    of one shape -- the library's cached workspace is per (device, stream), so the two streams never share packed
+    operands or split-K tickets (the reference allocates per call, op_mm.cuh:76-93).  Then the flat entry point on
+    the null stream beside them."""
+    L = qg.load()
+    cases = []
+    for i in range(2):
+        X, W = oracle.inputs(M, N, K, 140 + i)
+        cases.append((_dev(X, device), _dev(W, device), oracle.quantized_mm(X, W), torch.empty((M, N), device=device),
+                      torch.cuda.Stream(device)))
+    torch.cuda.synchronize()
+    for _ in range(6):
+        for Xd, Wd, _, O, s in cases:
+            assert L.op_mm_quantize_ex(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, O.data_ptr(), N, 1, M, N, K, 127.0,
+                                       s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    for i, (_, _, want, O, _) in enumerate(cases):
+        assert_bits_equal(O.cpu().numpy(), want, f"implicit workspace, stream {i}")
+    Xd, Wd, want, _, _ = cases[0]
+    O0 = torch.empty((M, N), device=device)
+    assert L.op_mm_quantize(Xd.data_ptr(), Wd.data_ptr(), O0.data_ptr(), M, N, K) == 0
+    torch.cuda.synchronize()
+    assert_bits_equal(O0.cpu().numpy(), want, "implicit workspace, null stream")
+
+
 def test_lds_dma_rings_repeat_race_screen(qg, oracle, device):
     """Race screen for the LDS-DMA rings that keep stages in flight across a raw s_barrier (the 3-stage
     64-tile int8 ring, with and without split-K, and the fp32 DMA ring): many back-to-back calls of each,
