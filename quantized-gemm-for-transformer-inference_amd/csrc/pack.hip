@@ -226,11 +226,15 @@ __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__r
         uint32_t mw0 = 0u;  // word 0: its bit 0 masks the absmax seed
         if constexpr (kMask) {
             static_assert(R <= 16, "the mask words cover len <= 4096");
-            int wj[R > 0 ? R : 1];
+            // the wave loads the mask once (lane l: words l and l + 64), then each lane takes its words by
+            // ds_bpermute: word (lane >> 3) + 8 j is < 64 exactly for j < 8
+            const int wl[2] = {lane, lane + 64};
+            uint32_t m2[2];
+            om->words(wl, m2);
 #pragma unroll
-            for (int j = 0; j < R; ++j) wj[j] = (lane >> 3) + 8 * j;
-            om->words(wj, mwd);
-            mw0 = om->word(0);
+            for (int j = 0; j < R; ++j)
+                mwd[j] = (uint32_t)__shfl((int)(j < 8 ? m2[0] : m2[1]), ((lane >> 3) + 8 * j) & 63, 64);
+            mw0 = __builtin_amdgcn_readlane(m2[0], 0);
         }
         if constexpr (kMask) {
             // outlier columns: X' holds +0 there (the seed included); branch-free selects
@@ -1033,11 +1037,15 @@ __device__ __forceinline__ void pack_w_strip8_body(int strip, const float *__res
     // loads
     uint32_t mw[4] = {0u, 0u, 0u, 0u}, mw0 = 0u;  // mw0: word 0, whose bit 0 masks the absmax seed
     if constexpr (kMask) {
-        int wi[4];
+        // the wave's 16 words (rq >> 3 = 4 wv .. 4 wv + 3, + 32 i) are loaded once, lane b + 4 i holding word
+        // 4 wv + b + 32 i, lane 16 word 0; each thread takes its 4 by ds_bpermute
+        const int b0 = (rq >> 3) - 4 * wv;
+        const int wl[1] = {lane < 16 ? 4 * wv + (lane & 3) + 32 * (lane >> 2) : (lane == 16 ? 0 : om->nwords)};
+        uint32_t m1[1];
+        om->words(wl, m1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wi[i] = (4 * rq + 1024 * i) >> 5;
-        om->words(wi, mw);
-        mw0 = om->word(0);
+        for (int i = 0; i < 4; ++i) mw[i] = (uint32_t)__shfl((int)m1[0], b0 + 4 * i, 64);
+        mw0 = __builtin_amdgcn_readlane(m1[0], 16);
     }
     bool seed_masked = false;
     if constexpr (kMask) {
