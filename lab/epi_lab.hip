@@ -4,7 +4,7 @@
 // then interleaved rounds time (a) the GEMM alone and (b) the whole drop-in call = product pack + variant GEMM, so a
 // store policy that leaves the output in the caches pays for it in the next call's pack, as in bench.py.
 //   build/epi_lab m n k rounds spec[,spec...]
-// spec = name of a row of the table in make() below
+// spec = name of a row of the table in make() below (ldsb*: lab/gemm_fm_ldsb.h, the B-through-LDS experiment)
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -14,6 +14,7 @@
 
 #include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
 #include "gemm_fm_epi.h"
+#include "gemm_fm_ldsb.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;
@@ -52,6 +53,12 @@ static Variant make(const std::string &s, int lib_wide) {
     if (s == "oct_m5") return {s, gemm_i8_fm_epi<5, 4, -1>, 0};
     if (s == "quad_m1") return {s, gemm_i8_fm_epi<1, 3, -1>, 0};
     if (s == "quad_m4") return {s, gemm_i8_fm_epi<4, 3, -1>, 0};
+    // lab/gemm_fm_ldsb.h (make_ldsb_fm.py): B through an LDS-DMA ring
+    if (s == "ldsb0") return {s, gemm_i8_fm_ldsb<0>, 0};
+    if (s == "ldsb1") return {s, gemm_i8_fm_ldsb<1>, 0};
+    if (s == "ldsb2") return {s, gemm_i8_fm_ldsb<2>, 0};
+    if (s == "row1k") return {s, gemm_i8_fm_epi<0, 5, -1>, 1};
+    if (s == "row1k_m1") return {s, gemm_i8_fm_epi<1, 5, -1>, 1};
     if (s == "nostore") return {s, gemm_i8_fm_epi<0, 2, -1>, 0};
     if (s == "nostore_m2") return {s, gemm_i8_fm_epi<2, 2, -1>, 0};
     if (s == "pairs_plain") return {s, gemm_i8_fm_epi<0, 1, 0>, 0};

@@ -13,6 +13,7 @@ VERDICT r05 item 1:
          2: no stores (the dequantize is computed and kept alive);
          3: 4 rows x 256 B per store: a 4 x 4 lane transpose (lanes c, c^4, c^8, c^12 over tiles 4g .. 4g+3, DPP);
          4: 2 rows x 512 B per store: an 8 x 8 lane transpose (lanes c ^ 1, 2, 4 over the 8 tiles, DPP)
+         5: (wide rows) the LDS image shared by the two waves of a tile-row half: one full 1-KiB tile row per store
   kAux  -1: __builtin_nontemporal_store (the product's `nt`), else the buffer-store aux bits (1 sc0, 2 nt, 16 sc1)
 Regenerate after changing the product kernel:  python3 lab/make_epi_fm.py"""
 import os
@@ -50,13 +51,13 @@ reps = [
     }
 """),
     ("    const bool image = full && p.wide_rows;\n",
-     "    const bool image = kStore == 0 && full && p.wide_rows;\n"
+     "    const bool image = (kStore == 0 || kStore == 5) && full && p.wide_rows;\n"
      "    float lab_sink = 0.0f;\n"
      "    const auto rsC = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0x7fffffff, 0x00020000);\n"),
     ("""#pragma unroll
             for (int np = 0; np < 4; ++np) {
                 const v4f o0 = tile_out(2 * np), o1 = tile_out(2 * np + 1);""",
-     """            if constexpr (kStore != 0) {
+     """            if constexpr (kStore != 0 && kStore != 5) {
                 if (full) {
                     lab_v4f q[8];
 #pragma unroll
@@ -115,6 +116,36 @@ reps = [
 }"""),
 ]
 for x, y in reps:
+    assert x in k, 'product kernel changed: update make_epi_fm.py (' + x[:50] + ')'
+    k = k.replace(x, y)
+
+reps += [
+    ("    float *T = sS + 2 * BM + 4 + wave * 64 * TS;  // this wave's image (wide rows)\n",
+     "    // kStore 5: the two waves of a tile-row half share one [64][TSX] image of 256 columns\n"
+     "    constexpr int TSX = kStore == 5 ? 260 : TS;\n"
+     "    float *T = kStore == 5 ? sS + 2 * BM + 4 + wm * 64 * TSX + wn * 128 : sS + 2 * BM + 4 + wave * 64 * TS;\n"),
+    ("""                    *reinterpret_cast<v4f *>(T + (16 * mq + c) * TS + 32 * np + 4 * kq) = o0;
+                    *reinterpret_cast<v4f *>(T + (16 * mq + c) * TS + 32 * np + 16 + 4 * kq) = o1;""",
+     """                    *reinterpret_cast<v4f *>(T + (16 * mq + c) * TSX + 32 * np + 4 * kq) = o0;
+                    *reinterpret_cast<v4f *>(T + (16 * mq + c) * TSX + 32 * np + 16 + 4 * kq) = o1;"""),
+    ("""        if (image) {
+            // wide rows: the half's 64 rows read back""",
+     """        if (kStore == 5 && image) {
+            // the pair's 64 rows x 256 columns: each wave stores 32 of them, one 1-KiB row per store, rotated order
+            __syncthreads();
+            const float *P = sS + 2 * BM + 4 + wm * 64 * TSX;
+            const int rot = __builtin_amdgcn_readfirstlane((tn * 7 + tm * 3) & 31);
+#pragma unroll 8
+            for (int it = 0; it < 32; ++it) {
+                const int rr = 2 * ((it + rot) & 31) + wn;
+                const v4f v = *reinterpret_cast<const v4f *>(P + rr * TSX + lane * 4);
+                __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(C + (int64_t)(gi0 + r0 + 64 * s + rr) * p.csh + gj0 + lane * 4));
+            }
+            __syncthreads();
+        } else if (image) {
+            // wide rows: the half's 64 rows read back"""),
+]
+for x, y in reps[-3:]:
     assert x in k, 'product kernel changed: update make_epi_fm.py (' + x[:50] + ')'
     k = k.replace(x, y)
 helpers = '''typedef float lab_v4f __attribute__((ext_vector_type(4)));
