@@ -8,6 +8,8 @@
 //   mask0    <4, true>, no outlier column       (the mask machinery alone: count 0)
 // Interleaved rounds, events around each launch; the outputs of mask / mask5 compared bit for bit.
 //   build/maskpack_lab [m n k rounds]
+// NOTE (round 6): written against the round-5 outlier.hip (per-stream accumulator slots, flags_acc); it does not build
+// against the current tree, whose fast path keeps no state between calls (git show bd71824:quantized-gemm-for-transformer-inference_amd/csrc/outlier.hip).
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
