@@ -25,7 +25,9 @@
  *     (device, stream) -- per calling thread as well for hipStreamPerThread -- so calls on
  *     different streams never share it; the reference allocates per call (op_mm.cuh:76-93).
  *     Growing it allocates (not allowed inside a hipGraph capture) and waits for that stream;
- *     pass an explicit workspace (op_mm_quantize_ws) for capture or to bound memory.
+ *     at most 8 such buffers are kept per device (the least recently used one is freed, after
+ *     a device synchronisation, when a ninth stream arrives).  Pass an explicit workspace
+ *     (op_mm_quantize_ws) for capture or to bound memory.
  */
 #ifndef QGEMM_H_
 #define QGEMM_H_

@@ -39,7 +39,11 @@ hipError_t pack_vectors(const float *src, int64_t row_stride, int64_t elem_strid
 // buffer is only reused in its stream's order, so calls on different streams never share packed operands or split-K
 // tickets (the reference allocates its temporaries per call, op_mm.cuh:76-93).  hipStreamPerThread names a different
 // stream in every host thread, so it is keyed by the calling thread as well.  Growth waits for the owning stream only.
+// At most kMaxCachedStreams buffers per (device, use): a process that cycles through many streams does not keep one
+// workspace per stream it ever used -- the least recently used buffer is freed after a device synchronisation (its
+// stream may no longer exist), which only happens when a new stream arrives.
 enum CacheUse { kUseWorkspace = 0, kUseSplitK = 1, kUseErrorStats = 2 };  // never shared: split-K tickets stay zero
+constexpr int kMaxCachedStreams = 8;
 struct CacheKey {
     int dev;
     hipStream_t stream;
@@ -55,9 +59,31 @@ struct CacheKey {
 struct CachedBuf {
     void *ptr = nullptr;
     size_t bytes = 0;
+    uint64_t last_use = 0;
 };
 std::mutex g_cache_mu;
 std::map<CacheKey, CachedBuf> g_cache;
+uint64_t g_cache_clock = 0;
+
+// frees the least recently used buffer of (dev, use) other than `keep` once there are more than kMaxCachedStreams
+hipError_t evict_cached(int dev, int use, const CacheKey &keep) {
+    int n = 0;
+    auto victim = g_cache.end();
+    for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
+        if (it->first.dev != dev || it->first.use != use) continue;
+        ++n;
+        if (!(it->first < keep) && !(keep < it->first)) continue;
+        if (victim == g_cache.end() || it->second.last_use < victim->second.last_use) victim = it;
+    }
+    if (n <= kMaxCachedStreams || victim == g_cache.end()) return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (victim->second.ptr) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+        e = hipFree(victim->second.ptr);
+    }
+    g_cache.erase(victim);
+    return e;
+}
 
 // zero_new: the buffer is zeroed when (re)allocated (split-K tickets start at zero; the launches re-zero them)
 hipError_t cached_buffer(size_t need, hipStream_t stream, int use, bool zero_new, size_t headroom, void **out) {
@@ -66,7 +92,11 @@ hipError_t cached_buffer(size_t need, hipStream_t stream, int use, bool zero_new
     if (e != hipSuccess) return e;
     const std::thread::id th = stream == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    CachedBuf &w = g_cache[CacheKey{dev, stream, th, use}];
+    const CacheKey key{dev, stream, th, use};
+    const bool fresh = g_cache.find(key) == g_cache.end();
+    CachedBuf &w = g_cache[key];
+    w.last_use = ++g_cache_clock;
+    if (fresh && (e = evict_cached(dev, use, key)) != hipSuccess) return e;
     if (w.bytes < need) {
         if (w.ptr) {
             // earlier calls on this stream may still be using it

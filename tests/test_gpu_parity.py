@@ -555,6 +555,28 @@ def test_implicit_workspace_two_streams(qg, oracle, device, M, N, K):
     assert_bits_equal(O0.cpu().numpy(), want, "implicit workspace, null stream")
 
 
+def test_implicit_workspace_many_streams(qg, oracle, device):
+    """The implicit workspace keeps at most 8 buffers per device: 12 streams, each running the implicit-workspace call
+    twice (the ninth and later streams evict the least recently used buffer), then all 12 again in reverse -- every
+    output bit-exact."""
+    L = qg.load()
+    M, N, K = 300, 520, 700
+    X, W = oracle.inputs(M, N, K, 151)
+    want = torch.from_numpy(oracle.quantized_mm(X, W)).to(device)
+    Xd, Wd = _dev(X, device), _dev(W, device)
+    streams = [torch.cuda.Stream(device) for _ in range(12)]
+    outs = [torch.full((M, N), float("nan"), device=device) for _ in streams]
+    torch.cuda.synchronize()
+    for order in (range(12), reversed(range(12))):
+        for i in order:
+            for _ in range(2):
+                assert L.op_mm_quantize_ex(Xd.data_ptr(), K, 1, Wd.data_ptr(), N, 1, outs[i].data_ptr(), N, 1, M, N, K,
+                                           127.0, streams[i].cuda_stream) == 0
+    torch.cuda.synchronize()
+    for i, O in enumerate(outs):
+        assert torch.equal(O.view(torch.int32), want.view(torch.int32)), f"stream {i}"
+
+
 def test_lds_dma_rings_repeat_race_screen(qg, oracle, device):
     """Race screen for the LDS-DMA rings that keep stages in flight across a raw s_barrier (the 3-stage
     64-tile int8 ring, with and without split-K, and the fp32 DMA ring): many back-to-back calls of each,
