@@ -53,8 +53,9 @@ def test_outlier_fast_path_bit_exact(qg, oracle, device, M, N, K, cols):
     assert_bits_equal(C.cpu().numpy(), want, f"outlier fast path {M}x{N}x{K}")
 
 
-# the fast path with many flag workgroups (16-row chunks since round 5: 512 / 516 chunks; M = 8257 also leaves a
-# partial last chunk), counts read back from the workspace
+# the fast path with many row splits of the column-mask launch (K = 128 / 256: 4 / 8 mask words, 16 splits of 512 rows
+# and 13 of 640 -- M = 8257 leaves a partial last split -- so the pack ORs up to 16 partial words per mask word), counts read
+# back from the workspace
 @pytest.mark.parametrize("M,N,K,cols", [(8192, 1280, 128, [0, 31, 32, 127]), (8257, 1280, 256, [1, 64, 200, 255])])
 def test_outlier_fast_path_many_chunks(qg, oracle, device, M, N, K, cols):
     X, W = _with_outliers(oracle, M, N, K, cols, 13)
