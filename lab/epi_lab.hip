@@ -57,6 +57,12 @@ static Variant make(const std::string &s, int lib_wide) {
     if (s == "ldsb0") return {s, gemm_i8_fm_ldsb<0>, 0};
     if (s == "ldsb1") return {s, gemm_i8_fm_ldsb<1>, 0};
     if (s == "ldsb2") return {s, gemm_i8_fm_ldsb<2>, 0};
+    // the product's map and image stores with other row-rotation formulas (make_epi_fm.py, kAux 100..104)
+    if (s == "rot0") return {s, gemm_i8_fm_epi<1, 0, 100>, 1};
+    if (s == "rot1") return {s, gemm_i8_fm_epi<1, 0, 101>, 1};
+    if (s == "rot2") return {s, gemm_i8_fm_epi<1, 0, 102>, 1};
+    if (s == "rot3") return {s, gemm_i8_fm_epi<1, 0, 103>, 1};
+    if (s == "rot4") return {s, gemm_i8_fm_epi<1, 0, 104>, 1};
     if (s == "row1k") return {s, gemm_i8_fm_epi<0, 5, -1>, 1};
     if (s == "row1k_m1") return {s, gemm_i8_fm_epi<1, 5, -1>, 1};
     if (s == "nostore") return {s, gemm_i8_fm_epi<0, 2, -1>, 0};

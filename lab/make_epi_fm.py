@@ -148,6 +148,16 @@ reps += [
 for x, y in reps[-3:]:
     assert x in k, 'product kernel changed: update make_epi_fm.py (' + x[:50] + ')'
     k = k.replace(x, y)
+
+# kAux >= 100 with kStore 0 (the product's image path): the per-tile row rotation formula of the wide-row stores
+#   100: none; 101: tn & 31; 102: (tm * 4 + tn) & 31; 103: (tn * 5 + tm * 9) & 31; 104: (tn * 7 + tm * 3) & 31 (rounds
+#   4-5; the product takes (tn * 13 + tm * 7) since round 6)
+rot_old = "            const int rot = __builtin_amdgcn_readfirstlane((tn * 13 + tm * 7) & 31);\n            const int c4 = (lane & 31) * 4;"
+assert rot_old in k, 'product kernel changed: update make_epi_fm.py (rotation)'
+k = k.replace(rot_old, """            const int rot = __builtin_amdgcn_readfirstlane(
+                kAux == 100 ? 0 : kAux == 101 ? (tn & 31) : kAux == 102 ? ((tm * 4 + tn) & 31)
+                : kAux == 103 ? ((tn * 5 + tm * 9) & 31) : kAux == 104 ? ((tn * 7 + tm * 3) & 31) : ((tn * 13 + tm * 7) & 31));
+            const int c4 = (lane & 31) * 4;""")
 helpers = '''typedef float lab_v4f __attribute__((ext_vector_type(4)));
 
 // lane c reads lane c ^ X of its 16-lane row (DPP; X = 4 as two bank-masked row shifts)

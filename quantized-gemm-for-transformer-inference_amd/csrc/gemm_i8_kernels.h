@@ -517,8 +517,10 @@ __global__ __launch_bounds__(kFmThreads, 1) void gemm_i8_fm(GemmArgs p) {
             // order) and stored as 512-B row segments, nontemporal: plain stores there leave the 128-MiB FFN-up output
             // in the caches and the next call's pack ran 15 us longer (same box, profiles/r05_ab_epilogue.log).  Each
             // tile starts its row-pair loop at its own offset (its rows otherwise meet the other tiles' on the same
-            // memory channels; lab/rot_lab.hip, round 4: 122.3 -> 117.8 us)
-            const int rot = __builtin_amdgcn_readfirstlane((tn * 7 + tm * 3) & 31);
+            // memory channels; lab/rot_lab.hip, round 4: 122.3 -> 117.8 us).  Round 6, with the 8-tile-row XCD patches
+            // (lab/epi_lab.hip rot*, profiles/r06_epi_lab.log run 4, both orders): (tn * 13 + tm * 7) 112.6 us against
+            // the round-4 formula (tn * 7 + tm * 3) 113.9-114.0, no rotation 117.0-117.3
+            const int rot = __builtin_amdgcn_readfirstlane((tn * 13 + tm * 7) & 31);
             const int c4 = (lane & 31) * 4;
 #pragma unroll 8
             for (int it = 0; it < 32; ++it) {
