@@ -106,8 +106,9 @@ __device__ __forceinline__ void build_index(const uint32_t *__restrict__ partial
 // of the chunk (16 float4 loads in flight per thread, 16 waves per CU), the groups' nibbles meet in LDS.  kAcc:
 // nonzero words are ORed into the call's accumulator (agent-scope atomics); else every word is stored
 // to partial[chunk][word] (sc1).  Then each workgroup, after every wave's stores / atomics have drained, arrives
-// on its XCD's counter (one lane, agent scope), and the last of each XCD on the global counter -- sharded, because ≈ 12 ns per arrival serialise on one counter (MI355X_MICROARCH.md fan-in row);
-// the write-through hand-off of the sc1 table, row 1, at each level.  The workgroup that arrives last overall
+// on its XCD's counter (one lane, agent scope), and the last of each XCD on the global counter -- sharded, because
+// ≈ 12 ns per arrival serialise on one counter (MI355X_MICROARCH.md fan-in row); the write-through hand-off of the
+// sc1 table, row 1, at each level.  The workgroup that arrives last overall
 // builds the column mask, ranks, list and count (build_index over the accumulator or the partial words) -- no
 // separate index launch.
 constexpr int kFlagThreads = 1024, kFlagGroups = 4, kGroupRows = kChunkRows / kFlagGroups;
