@@ -84,24 +84,32 @@ int main(int argc, char **argv) {
                same(v.q, v2.q, v.rows_pad * v.k_pad), same(v.scale, v2.scale, v.rows_pad * 4));
         hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
         if (w <= 1024) {  // the LDS-walking chain in the same register-resident kernel
-            add_layernorm_rows_vec_kernel<true, 4, 0, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, sizeof(float) * 4 * w>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+            add_layernorm_rows_vec_kernel<true, 4, 0, false, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, sizeof(float) * 4 * w>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
             CK(hipDeviceSynchronize());
             printf("hop chain vs LDS chain: Y %s  q %s  scale %s\n", same(Y2, Y3, (size_t)rows * w * 4),
                    same(v.q, v2.q, v.rows_pad * v.k_pad), same(v.scale, v2.scale, v.rows_pad * 4));
         }
-        for (int var = 0; var < 3; ++var) {
-            if (var == 2 && w > 1024) break;
+        if (w <= 1024) {  // the round-3..6 interleaved layout (one hop per 4 elements)
+            add_layernorm_rows_vec_kernel<true, 4, 0, true, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, 0>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+            CK(hipDeviceSynchronize());
+            printf("block hops vs interleaved hops: Y %s  q %s  scale %s\n", same(Y2, Y3, (size_t)rows * w * 4),
+                   same(v.q, v2.q, v.rows_pad * v.k_pad), same(v.scale, v2.scale, v.rows_pad * 4));
+        }
+        for (int rep = 0; rep < 3; ++rep)
+        for (int var = 0; var < 4; ++var) {
+            if (var >= 2 && w > 1024) break;
             std::vector<float> ts;
             for (int it = 0; it < 30; ++it) {
                 CK(hipEventRecord(e0));
                 if (var == 0) CK(launch_add_layernorm_rows_pack(A, B, Y2, rows, w, 127.0f, v, nullptr));
-                else if (var == 2) add_layernorm_rows_vec_kernel<true, 4, 0, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, sizeof(float) * 4 * w>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+                else if (var == 3) add_layernorm_rows_vec_kernel<true, 4, 0, true, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, 0>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
+                else if (var == 2) add_layernorm_rows_vec_kernel<true, 4, 0, false, false><<<(unsigned)((v2.rows_pad + 3) / 4), 256, sizeof(float) * 4 * w>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
                 else add_layernorm_rows_kernel<true><<<(unsigned)((v2.rows_pad + 3) / 4), 256, lds>>>(A, B, Y3, rows, w, v2.q, v2.scale, v2.k_pad, v2.rows_pad, 127.0f);
                 CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
                 float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms * 1000);
             }
             std::sort(ts.begin(), ts.end());
-            const char *nm[3] = {"vector (hop chain)", "scalar", "vector (LDS chain)"};
+            const char *nm[4] = {"vector (block hops, product)", "scalar", "vector (LDS chain)", "vector (interleaved hops)"};
             printf("%s kernel: median %.2f us\n", nm[var], ts[ts.size() / 2]);
         }
     }

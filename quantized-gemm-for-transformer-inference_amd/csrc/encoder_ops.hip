@@ -82,6 +82,40 @@ __device__ __forceinline__ float lane_chain_sum(const float4 (&x)[kV], int w4) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), last));
 }
 
+// The same chain over the block layout: lane l holds the kV consecutive float4 columns kV l .. kV l + kV - 1
+// (elements 4 kV l .. 4 kV (l + 1) - 1), so the running sum hops once per 4 kV elements instead of once per 4:
+// step t is one v_add_f32 on the left neighbour's sum, then 4 kV - 1 in-lane adds, and after step t lane t - 1
+// holds the chain through its own block (the induction of lane_chain_sum).  nl = the lanes that hold elements
+// (<= 64); elements past the row must be -0.0f (x + -0 == x for every x, -0 and NaN included), so the last
+// lane's adds stay uniform.  Each hop costs the DPP read's wait states on top of its add: 16-element blocks
+// spend ~4.5 cycles per element against ~6 for lane_chain_sum's 4.
+template <int kV>
+__device__ __forceinline__ float block_step(float s, const float4 (&x)[kV]) {
+    s = __fadd_rn(hop_left(s), x[0].x);
+    s = __fadd_rn(s, x[0].y);
+    s = __fadd_rn(s, x[0].z);
+    s = __fadd_rn(s, x[0].w);
+#pragma unroll
+    for (int i = 1; i < kV; ++i) {
+        s = __fadd_rn(s, x[i].x);
+        s = __fadd_rn(s, x[i].y);
+        s = __fadd_rn(s, x[i].z);
+        s = __fadd_rn(s, x[i].w);
+    }
+    return s;
+}
+template <int kV>
+__device__ __forceinline__ float lane_block_sum(const float4 (&x)[kV], int nl) {
+    float s = 0.0f;
+    int t = 0;
+    for (; t + 4 <= nl; t += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s = block_step<kV>(s, x);
+    }
+    for (; t < nl; ++t) s = block_step<kV>(s, x);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), nl - 1));
+}
+
 // fl((x - mean)^2): pow(x - mean, 2) as fp32 d*d (CUDA's float pow(float, int) overload)
 __device__ __forceinline__ float sq_dev(float x, float mean) {
     const float d = __fsub_rn(x, mean);
@@ -201,16 +235,20 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_kernel(cons
     stamp(6);
 }
 
-// The same add + layernorm (+ pack) for rows of w % 4 == 0 floats, 16-B aligned: each lane holds its
-// columns 4j..4j+3 (j = lane + 64 i, i < kV) in registers from the first load to the last use, so
-// neither the normalisation nor the pack re-reads A, B or LDS; each packed dword is
-// one lane's four columns.
-// kHop (the product): both sums as lane_chain_sum over the registers; false: staged in LDS and walked by
-// seq_sum (lab comparison)
-template <bool kPack, int kV, int kStamp = 0, bool kHop = true>
+// The same add + layernorm (+ pack) for rows of w % 4 == 0 floats, 16-B aligned: each lane holds kV float4
+// columns (columns 4j..4j+3 of float4 column j, layout below) in registers from the first load to the last
+// use, so neither the normalisation nor the pack re-reads A, B or LDS; each packed dword is one lane's four
+// columns.
+// kHop (the product): both sums hop lane to lane over the registers; false: staged in LDS and walked by
+// seq_sum (lab comparison).  kBlk (the product): lane l holds the float4 columns j = kV l + i (a block of 4 kV
+// consecutive elements, lane_block_sum: one hop per block, and each lane's packed dwords of a 16-element
+// block are one 16-B piece of the fragment-major row); false: j = lane + 64 i (lane_chain_sum, one hop per 4
+// elements; the round-3 to round-6 product, kept for the lab comparison)
+template <bool kPack, int kV, int kStamp = 0, bool kHop = true, bool kBlk = true>
 __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     const float *__restrict__ A, const float *__restrict__ B, float *__restrict__ Y, int64_t rows, int w,
     int8_t *__restrict__ q, float *__restrict__ qscale, int64_t k_pad, int64_t rows_pad, float range) {
+    static_assert(!kBlk || kHop, "the block layout has no LDS-walking form");
     extern __shared__ __attribute__((aligned(16))) float stage[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
@@ -230,11 +268,13 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     const float4 *a = reinterpret_cast<const float4 *>(A + row * w), *b = reinterpret_cast<const float4 *>(B + row * w);
     float4 *y = reinterpret_cast<float4 *>(Y + row * w);
     float *st = stage + wv * w;
+    auto col = [&](int i) __attribute__((always_inline)) { return kBlk ? kV * lane + i : lane + 64 * i; };
+    const int nl = (w4 + kV - 1) / kV;  // kBlk: the lanes that hold elements
     float4 x[kV];
 #pragma unroll
     for (int i = 0; i < kV; ++i) {
-        const int j = lane + 64 * i;
-        x[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const int j = col(i);
+        x[i] = kBlk ? make_float4(-0.0f, -0.0f, -0.0f, -0.0f) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (j < w4) {
             const float4 av = a[j], bv = b[j];
             x[i] = make_float4(__fadd_rn(av.x, bv.x), __fadd_rn(av.y, bv.y), __fadd_rn(av.z, bv.z),
@@ -248,7 +288,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     }
     stamp(1);
     const float fw = (float)w;
-    const float mean = __fdiv_rn(kHop ? lane_chain_sum<kV>(x, w4) : seq_sum(st, w), fw);  // op_layernorm.cuh:15-19
+    const float sum_x = kBlk ? lane_block_sum<kV>(x, nl) : kHop ? lane_chain_sum<kV>(x, w4) : seq_sum(st, w);
+    const float mean = __fdiv_rn(sum_x, fw);  // op_layernorm.cuh:15-19
     stamp(2);
     // the squared deviations, formed from the registers (a chain that formed them itself would carry the
     // sub -> mul latency on every add: measured 2x slower)
@@ -256,10 +297,12 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     if constexpr (kHop) {
         float4 d[kV];
 #pragma unroll
-        for (int i = 0; i < kV; ++i)
+        for (int i = 0; i < kV; ++i) {
             d[i] = make_float4(sq_dev(x[i].x, mean), sq_dev(x[i].y, mean), sq_dev(x[i].z, mean), sq_dev(x[i].w, mean));
+            if (kBlk && col(i) >= w4) d[i] = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);  // past the row: the identity
+        }
         stamp(3);
-        var = __fdiv_rn(lane_chain_sum<kV>(d, w4), fw);            // :21-25
+        var = __fdiv_rn(kBlk ? lane_block_sum<kV>(d, nl) : lane_chain_sum<kV>(d, w4), fw);  // :21-25
     } else {
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -278,7 +321,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     float cand = -INFINITY;
 #pragma unroll
     for (int i = 0; i < kV; ++i) {
-        const int j = lane + 64 * i;
+        const int j = col(i);
         if (j < w4) {
             float4 v;                                                // (x - mean) / var (:28), as written
             v.x = __fdiv_rn(__fsub_rn(x[i].x, mean), var);
@@ -303,12 +346,29 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
         const float cx = absmax_finish(seed, cand);
         const float sc = inv_divide(range, cx);
         auto qrow = [&](int64_t c) __attribute__((always_inline)) -> uint32_t & { return *qword(q, row, 4 * c, k_pad); };  // fragment-major q
+        uint32_t pk[kV];
 #pragma unroll
-        for (int i = 0; i < kV; ++i) {
-            const int j = lane + 64 * i;
-            if (j < w4)
-                qrow(j) = (uint32_t)(quant_i8(x[i].x, sc) & 0xff) | ((uint32_t)(quant_i8(x[i].y, sc) & 0xff) << 8) |
-                          ((uint32_t)(quant_i8(x[i].z, sc) & 0xff) << 16) | ((uint32_t)(quant_i8(x[i].w, sc) & 0xff) << 24);
+        for (int i = 0; i < kV; ++i)
+            pk[i] = (uint32_t)(quant_i8(x[i].x, sc) & 0xff) | ((uint32_t)(quant_i8(x[i].y, sc) & 0xff) << 8) |
+                    ((uint32_t)(quant_i8(x[i].z, sc) & 0xff) << 16) | ((uint32_t)(quant_i8(x[i].w, sc) & 0xff) << 24);
+        if constexpr (kBlk) {
+            // dwords kV l + 4g .. + 3 = k 16 (kV l / 4 + g) .. + 15: one aligned 16-B piece of the row
+#pragma unroll
+            for (int g = 0; g < kV / 4; ++g) {
+                const int j0 = col(4 * g);
+                if (j0 + 3 < w4) {
+                    *reinterpret_cast<uint4 *>(qword(q, row, 4 * j0, k_pad)) =
+                        make_uint4(pk[4 * g], pk[4 * g + 1], pk[4 * g + 2], pk[4 * g + 3]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j0 + e < w4) qrow(j0 + e) = pk[4 * g + e];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kV; ++i)
+                if (col(i) < w4) qrow(col(i)) = pk[i];
         }
         for (int64_t c4 = w4 + lane; c4 < k_pad / 4; c4 += 64) qrow(c4) = 0u;  // padding columns
         if (lane == 0) qscale[row] = cx;
