@@ -181,17 +181,18 @@ __device__ __forceinline__ void outlier_column_list(const OutlierMask &om, int *
 // ------------------------------------------------------------------------------------------------
 // pack_rows, vector path: rows of `len` floats at src + r*sh, unit inner stride, 16-B aligned rows.
 // R > 0: each lane keeps R float4 chunks in registers (len <= 256*R), one HBM read.
-// R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = 4-row group index.
+// R == 0: two streaming passes (second pass mostly L2 hits).  `blk` = kGroup-row group index.
 // kStage: the packed row goes to `stage` (the wave's LDS row, dword c at stage[c]) instead of q; the caller
 // writes the block's staged rows out as whole 128-B lines of the fragment-major q (write_staged_rows).
-template <int R, bool kMask = false, bool kWT = false, bool kStage = false>
+// kGroup: rows per `blk` (wave w of the block takes row blk * kGroup + w).
+template <int R, bool kMask = false, bool kWT = false, bool kStage = false, int kGroup = 4>
 __device__ __forceinline__ void pack_rows_vec_body(int64_t blk, const float *__restrict__ src, int64_t sh, int rows,
                                                    int len, float range, float *__restrict__ scale,
                                                    int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad,
                                                    const OutlierMask *om = nullptr, uint32_t *stage = nullptr) {
     static_assert(!kMask || R > 0, "the outlier mask needs the register-resident rows");
     const int lane = threadIdx.x & 63;
-    const int64_t row = blk * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const int64_t row = blk * kGroup + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     if (row >= rows_pad) return;
     // dword c of the packed row (k = 4c), fragment-major layout (qgemm_internal.h fofs), or of the LDS stage
     auto put = [&](int64_t c, uint32_t v) __attribute__((always_inline)) {
@@ -408,6 +409,18 @@ __global__ __launch_bounds__(R > 0 ? 512 : 256) void pack_rows_vec_kernel(const 
     } else {
         pack_rows_vec_body<R>(b, src, sh, rows, len, range, scale, q, rows_pad, k_pad);
     }
+}
+
+// R > 0 with fewer staged 8-row blocks than CUs (rows_pad < 2 048: the encoder's activations): 2 rows per 128-thread
+// block, each wave's dwords stored straight into the fragment-major q -- 4x the blocks, so 4x the CUs pull rows
+// (lab/rowpack_lab.hip, profiles/r06_rowpack_lab.log: 512 x 4 096 4.28 vs 5.38 us, 512 x 1 024 3.03-3.15 vs 3.23 us;
+// at 2 048 rows the staged lines are as fast or faster)
+template <int R>
+__global__ __launch_bounds__(128) void pack_rows_pair_kernel(const float *__restrict__ src, int64_t sh, int rows, int len,
+                                                             float range, float *__restrict__ scale,
+                                                             int8_t *__restrict__ q, int64_t rows_pad, int64_t k_pad) {
+    pack_rows_vec_body<R, false, false, false, 2>(xcd_contig(blockIdx.x, 0, gridDim.x), src, sh, rows, len, range, scale,
+                                                  q, rows_pad, k_pad);
 }
 
 // pack_rows, generic strides (any sh, sw): scalar loads, two passes.
@@ -1218,9 +1231,14 @@ hipError_t launch_pack_rows(const float *src, int64_t sh, int64_t sw, int rows, 
                                                              out.rows_pad, out.k_pad);
         return hipGetLastError();
     }
-#define QG_ROWS(Rv)                                                                                               \
-    pack_rows_vec_kernel<Rv><<<(Rv) > 0 ? (unsigned)(out.rows_pad / 8) : grid.x, (Rv) > 0 ? 512 : 256, 0, stream>>>( \
-        src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad)
+    const bool pairs = out.rows_pad < 2048;  // fewer than 256 staged 8-row blocks
+#define QG_ROWS(Rv)                                                                                                   \
+    if ((Rv) > 0 && pairs)                                                                                            \
+        pack_rows_pair_kernel<((Rv) > 0 ? (Rv) : 1)><<<(unsigned)(out.rows_pad / 2), 128, 0, stream>>>(                 \
+            src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad);                                    \
+    else                                                                                                              \
+        pack_rows_vec_kernel<Rv><<<(Rv) > 0 ? (unsigned)(out.rows_pad / 8) : grid.x, (Rv) > 0 ? 512 : 256, 0, stream>>>( \
+            src, sh, rows, len, range, out.scale, out.q, out.rows_pad, out.k_pad)
     if (rows_regs(len) < 0) {
         pack_rows_block_kernel<<<(unsigned)out.rows_pad, 256, 0, stream>>>(src, sh, rows, len, range, out.scale, out.q,
                                                                            out.rows_pad, out.k_pad);
