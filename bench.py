@@ -34,6 +34,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -95,6 +96,10 @@ def parse(argv=None):
                    help="how the GEMM kernel is timed inside the timed region: hipExtLaunchKernel start/stop "
                         "events (ext, exact kernel bounds), hipEventRecord around its launch (record, includes the "
                         "kernel-boundary gap), or not at all (none)")
+    p.add_argument("--node-timeout", type=float, default=120.0,
+                   help="seconds the c4_node report may take (its RCCL collectives have never run at N > 1 on this "
+                        "pool): past it rank 0 prints the measurement line with c4_node marked as timed out and every "
+                        "rank exits (0 = no watchdog)")
     p.add_argument("--node-chunks", type=int, default=0,
                    help="row chunks per rank of the pipelined whole-node C4 step (0 = rows / 4096, at least 1)")
     p.add_argument("--launch-dry-run", action="store_true",
@@ -375,6 +380,36 @@ def c4_node_report(args, world, rows, distributed, dev, serial_step, reset, pipe
         "note": "the compute is a full drop-in call per rank on its row shard (pack + GEMM); world 1: the whole "
                 "65536-row problem on one GPU and a no-op gather",
     }
+
+
+def run_with_deadline(fn, seconds, on_timeout):
+    """fn() under a watchdog: if it has not returned after `seconds`, on_timeout() runs on the watchdog thread and the
+    process ends with os._exit(0), so a collective that never completes (a peer that never arrives) cannot hold back the
+    measurement line that is already complete.  seconds <= 0: no watchdog.  Each rank arms its own."""
+    if seconds <= 0:
+        return fn()
+    lock = threading.Lock()
+    state = {"done": False}
+
+    def fire():
+        with lock:
+            if state["done"]:
+                return
+            try:
+                on_timeout()
+            finally:
+                sys.stdout.flush()
+                os._exit(0)
+
+    timer = threading.Timer(seconds, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        return fn()
+    finally:
+        with lock:
+            state["done"] = True
+        timer.cancel()
 
 
 def c4_node(args, qg, dev, world, rank, distributed, comm):
@@ -675,7 +710,15 @@ def bench_gemm(args, qg, L, dev, world, rank, distributed, comm, rccl_world):
         "prewarm": prewarm,
     })
     if args.config == "c2" and args.node_reps > 0:
-        node = c4_node(args, qg, dev, world, rank, distributed, comm)
+        def node_timed_out():
+            if rank == 0:
+                result["c4_node"] = {"error": f"did not finish within {args.node_timeout:g} s (an RCCL collective "
+                                              "that never completed); every other field of this line was measured "
+                                              "before it"}
+                print(json.dumps(result), flush=True)
+
+        node = run_with_deadline(lambda: c4_node(args, qg, dev, world, rank, distributed, comm), args.node_timeout,
+                                 node_timed_out)
         result["c4_node"] = node
         result["allgather_ms_median"] = node["allgather_ms_median"]
     if rank == 0 and args.cold_steps > 0:

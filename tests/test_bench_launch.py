@@ -99,3 +99,39 @@ def test_main_distributed_branch_world2_gloo(tmp_path):
     assert js["ms_per_step"] >= 40.0
     assert abs(js["value"] - 2 * 1e3 / js["ms_per_step"]) / js["value"] < 1e-3
     assert js["metric"].startswith("int8 GEMMs/sec") and js["scaling"] == "weak"
+
+
+_DEADLINE_SCRIPT = r"""
+import json, sys, time
+sys.path.insert(0, {repo!r})
+import bench
+result = {{"metric": "m", "value": 1.0}}
+def hang():
+    time.sleep(60)  # a collective that never completes
+def timed_out():
+    result["c4_node"] = {{"error": "timed out"}}
+    print(json.dumps(result), flush=True)
+bench.run_with_deadline(hang, 1.0, timed_out)
+print("not reached", flush=True)
+"""
+
+
+def test_node_watchdog_prints_the_line_and_exits():
+    """bench.run_with_deadline (the c4_node guard): a step that never returns is cut off after the deadline; the
+    timeout hook's JSON line is the process's output and the exit status is 0."""
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", _DEADLINE_SCRIPT.format(repo=REPO)], env=_env(), capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1 and json.loads(lines[0]) == {"metric": "m", "value": 1.0, "c4_node": {"error": "timed out"}}
+    assert time.time() - t0 < 30
+
+
+def test_node_watchdog_passes_results_through():
+    import bench
+    fired = []
+    assert bench.run_with_deadline(lambda: {"ok": 1}, 5.0, lambda: fired.append(1)) == {"ok": 1}
+    assert bench.run_with_deadline(lambda: 7, 0, lambda: fired.append(1)) == 7
+    time.sleep(0.1)
+    assert not fired
