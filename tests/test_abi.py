@@ -339,3 +339,25 @@ def test_chunked_allgather_plan_assembles_every_rank(qg, world, chunks):
         for b in bufs:
             assert np.array_equal(b, np.arange(m * n, dtype=float))
         assert len(plan) <= world * chunks
+
+
+@pytest.mark.parametrize("m,n,k,tile,splits", [
+    (4096, 4096, 4096, 256, 1),     # C2: 256 tiles, one per CU
+    (2048, 16384, 4096, 256, 1),    # C3 FFN up: 512 tiles
+    (2048, 4096, 16384, 256, 2),    # C3 FFN down: 128 tiles, ticket-first 2-way split-K
+    (8192, 4096, 4096, 256, 1),     # C4 shard
+    (512, 3072, 1024, 64, 1),       # C5 Q/K/V (384 64-tiles)
+    (512, 4096, 1024, 64, 1),       # C5 FFN up (512 64-tiles)
+    (512, 1024, 1024, 32, 1),       # C5 W_O (512 32-tiles)
+    (512, 1024, 4096, 32, 1),       # C5 FFN down (512 32-tiles)
+    (128, 128, 128, 64, 1),         # C1: 4 64-tiles (too few 32-tiles to fill the chip)
+])
+def test_gemm_plan_for_every_baseline_shape(qg, m, n, k, tile, splits):
+    """qgemm_gemm_plan (host-only: no GPU) picks, for each BASELINE config's GEMM shapes, the kernel the profiles in
+    profiles/r06_kernel_stats_*.csv show running (gemm_i8.hip gemm_plan)."""
+    L = qg.load()
+    t, name = ctypes.c_int(0), ctypes.c_char_p()
+    assert L.qgemm_gemm_plan(m, n, k, ctypes.byref(t), ctypes.byref(name)) == splits
+    assert t.value == tile
+    expect = "gemm_i8_fm" if tile == 256 else f"gemm_i8_small<{tile}>"
+    assert name.value.decode().startswith(expect)
