@@ -249,6 +249,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void add_layernorm_rows_vec_kernel(
     const float *__restrict__ A, const float *__restrict__ B, float *__restrict__ Y, int64_t rows, int w,
     int8_t *__restrict__ q, float *__restrict__ qscale, int64_t k_pad, int64_t rows_pad, float range) {
     static_assert(!kBlk || kHop, "the block layout has no LDS-walking form");
+    static_assert(!kBlk || kV % 4 == 0, "the block layout stores whole 16-B pieces of the packed row");
     extern __shared__ __attribute__((aligned(16))) float stage[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row = (int64_t)blockIdx.x * kRowWaves + wv;
