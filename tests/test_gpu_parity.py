@@ -619,3 +619,37 @@ def test_fm_short_k_l2_hot_repeat(qg, oracle, device, K):
     torch.cuda.synchronize()
     for i, O in enumerate(outs):
         assert_bits_equal(O.cpu().numpy(), want, f"4096x4096x{K} repeat {i}")
+
+
+def _fuzz_shapes(count=24, seed=20261018):
+    """Seeded shapes, M, N in [1, 700], K in [1, 2100] (the oracle finishes each in well under a second): every other
+    one log-uniform (small, ragged), the rest uniform over the upper range, and every sixth with K = 1, M = 1 or N = 1."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        if i % 2:  # log-uniform: mostly small, ragged sizes
+            M, N, K = (int(round(np.exp(rng.uniform(0.0, np.log(hi))))) for hi in (700, 700, 2100))
+        else:      # uniform in the upper three quarters: several tiles and k-steps
+            M, N, K = (int(rng.integers(hi // 4, hi + 1)) for hi in (700, 700, 2100))
+        if i % 6 == 1:
+            K = 1
+        elif i % 6 == 2:
+            M = 1
+        elif i % 6 == 3:
+            N = 1
+        out.append((max(1, M), max(1, N), max(1, K)))
+    return out
+
+
+@pytest.mark.parametrize("M,N,K", _fuzz_shapes())
+def test_seeded_shape_fuzz(qg, oracle, device, M, N, K):
+    """Shapes drawn from a fixed seed (not hand-picked), each through the drop-in call against the full oracle, with
+    the absmax seed quirk planted in a few rows and columns and a NaN and an inf in X when it has room."""
+    X, W = oracle.inputs(M, N, K, 71 + M + N + K)
+    if K > 1:
+        X[::7, 0] = -1.5   # rows whose signed first element is the largest magnitude
+        W[0, ::5] = -1.25
+    if M * K > 8:
+        X[M // 2, K // 2] = np.nan
+        X[M - 1, K - 1] = np.inf
+    assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"fuzz {M}x{N}x{K}")
