@@ -15,6 +15,7 @@
 #include "../quantized-gemm-for-transformer-inference_amd/csrc/pack.hip"
 #include "gemm_fm_epi.h"
 #include "gemm_fm_ldsb.h"
+#include "gemm_fm_tile.h"
 
 using namespace qgemm;
 using namespace qgemm::gemm;
@@ -31,6 +32,7 @@ struct Variant {
     std::string name;
     KernelFn fn;
     int wide;  // GemmArgs.wide_rows
+    int tmsz = 256, tnsz = 256;  // workgroup tile (lab/gemm_fm_tile.h: kTM x kTN)
 };
 
 static Variant make(const std::string &s, int lib_wide) {
@@ -77,6 +79,18 @@ static Variant make(const std::string &s, int lib_wide) {
     if (s == "quad_m2") return {s, gemm_i8_fm_epi<2, 3, -1>, 0};
     if (s == "oct") return {s, gemm_i8_fm_epi<0, 4, -1>, 0};
     if (s == "oct_m2") return {s, gemm_i8_fm_epi<2, 4, -1>, 0};
+    // lab/gemm_fm_tile.h (make_tile_fm.py): workgroup tile kTM x kTN, XCD patches of kGM tile-rows; _img / _pairs = the
+    // wide-row LDS-image stores / the paired register stores
+    if (s == "t256_g8_img") return {s, gemm_i8_fm_tile<256, 256, 8>, 1, 256, 256};
+    if (s == "t256_g4_pairs") return {s, gemm_i8_fm_tile<256, 256, 4>, 0, 256, 256};
+    if (s == "t128x512_g4_img") return {s, gemm_i8_fm_tile<128, 512, 4>, 1, 128, 512};
+    if (s == "t128x512_g8_img") return {s, gemm_i8_fm_tile<128, 512, 8>, 1, 128, 512};
+    if (s == "t128x512_g16_img") return {s, gemm_i8_fm_tile<128, 512, 16>, 1, 128, 512};
+    if (s == "t128x512_g4_pairs") return {s, gemm_i8_fm_tile<128, 512, 4>, 0, 128, 512};
+    if (s == "t128x512_g8_pairs") return {s, gemm_i8_fm_tile<128, 512, 8>, 0, 128, 512};
+    if (s == "t128x512_g16_pairs") return {s, gemm_i8_fm_tile<128, 512, 16>, 0, 128, 512};
+    if (s == "t512x128_g2_pairs") return {s, gemm_i8_fm_tile<512, 128, 2>, 0, 512, 128};
+    if (s == "t512x128_g4_pairs") return {s, gemm_i8_fm_tile<512, 128, 4>, 0, 512, 128};
     printf("unknown variant %s\n", s.c_str());
     exit(2);
 }
@@ -114,12 +128,22 @@ int main(int argc, char **argv) {
     CK(hipDeviceSynchronize());
     std::vector<float> href((size_t)m * n), hgot((size_t)m * n);
     CK(hipMemcpy(href.data(), Cref, href.size() * 4, hipMemcpyDeviceToHost));
-    auto args = [&](const Variant &v) { GemmArgs q = p; q.C = C; q.wide_rows = v.wide; return q; };
+    auto args = [&](const Variant &v) {
+        GemmArgs q = p;
+        q.C = C;
+        q.wide_rows = v.wide;
+        q.tiles_m = m / v.tmsz;
+        q.tiles_n = n / v.tnsz;
+        return q;
+    };
+    auto vgrid = [&](const Variant &v) { return dim3((m / v.tmsz) * (n / v.tnsz)); };
+    for (auto &v : vs)
+        if (m % v.tmsz || n % v.tnsz) { printf("%s: %d x %d is not a whole number of %d x %d tiles\n", v.name.c_str(), m, n, v.tmsz, v.tnsz); return 2; }
     for (auto &v : vs) {
         if (v.name.rfind("nostore", 0) == 0) continue;
         for (int rep = 0; rep < 2; ++rep) {
             CK(hipMemset(C, 0xff, (size_t)m * n * 4));
-            v.fn<<<grid, 256>>>(args(v));
+            v.fn<<<vgrid(v), 256>>>(args(v));
             CK(hipDeviceSynchronize());
             CK(hipMemcpy(hgot.data(), C, hgot.size() * 4, hipMemcpyDeviceToHost));
             size_t bad = 0;
@@ -135,15 +159,16 @@ int main(int argc, char **argv) {
     for (int r = 0; r < rounds; ++r)
         for (size_t vi = 0; vi < vs.size(); ++vi) {
             const GemmArgs q = args(vs[vi]);
-            for (int w = 0; w < 3; ++w) vs[vi].fn<<<grid, 256>>>(q);
+            const dim3 g = vgrid(vs[vi]);
+            for (int w = 0; w < 3; ++w) vs[vi].fn<<<g, 256>>>(q);
             CK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) vs[vi].fn<<<grid, 256>>>(q);
+            for (int i = 0; i < reps; ++i) vs[vi].fn<<<g, 256>>>(q);
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
             tg[vi].push_back(ms * 1000 / reps);
-            for (int w = 0; w < 2; ++w) { pack(); vs[vi].fn<<<grid, 256>>>(q); }
+            for (int w = 0; w < 2; ++w) { pack(); vs[vi].fn<<<g, 256>>>(q); }
             CK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) { pack(); vs[vi].fn<<<grid, 256>>>(q); }
+            for (int i = 0; i < reps; ++i) { pack(); vs[vi].fn<<<g, 256>>>(q); }
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             CK(hipEventElapsedTime(&ms, e0, e1));
             tc[vi].push_back(ms * 1000 / reps);
