@@ -307,6 +307,26 @@ def test_full_size_every_output(qg, oracle, device, M, N, K, cfg):
     assert_bits_equal(O.cpu().numpy(), oracle.quantized_mm(Xh, Wh), f"{cfg} {M}x{N}x{K} full output")
 
 
+def test_output_past_2_31_elements(qg, oracle, device):
+    """A 65536 x 36864 output (2.42e9 elements, 9.7 GB: element offsets past 2^31) from K = 128: the sampled rows whose
+    offsets row * N exceed 2^31, the last row and a few below it, bit for bit against the oracle's row restatement
+    (its Cw over the whole W).  Exercises the 64-bit output addressing of the epilogue at a size the 288-GB HBM holds."""
+    M, N, K = 65536, 36864, 128
+    X = qg.fill_uniform(torch.empty((M, K), device=device), seed=2 * 53)
+    W = qg.fill_uniform(torch.empty((K, N), device=device), seed=2 * 53 + 1)
+    O = torch.full((M, N), float("nan"), device=device)
+    torch.cuda.synchronize()
+    assert qg.load().op_mm_quantize(X.data_ptr(), W.data_ptr(), O.data_ptr(), M, N, K) == 0
+    torch.cuda.synchronize()
+    first_past = (1 << 31) // N + 1  # the first row whose every element lies past 2^31
+    rows = np.unique(np.concatenate([[0, first_past - 1, first_past, M - 1],
+                                     np.linspace(first_past, M - 1, 28).astype(np.int64)]))
+    got = O[torch.from_numpy(rows).to(device)].cpu().numpy()
+    del O
+    Xh, Wh = oracle.uniform((M, K), 2 * 53), oracle.uniform((K, N), 2 * 53 + 1)
+    assert_bits_equal(got, oracle.quantized_mm_rows(Xh, Wh, rows.astype(np.int32)), f"{M}x{N}x{K} rows past 2^31")
+
+
 def test_strided_views(qg, oracle, device):
     """Transposed and sliced views, as the reference's Index() macro allows (tensor.cuh:121-149)."""
     M, N, K = 200, 150, 260
