@@ -327,6 +327,48 @@ def test_output_past_2_31_elements(qg, oracle, device):
     assert_bits_equal(got, oracle.quantized_mm_rows(Xh, Wh, rows.astype(np.int32)), f"{M}x{N}x{K} rows past 2^31")
 
 
+def _uniform_rows(seed, rows, K):
+    """Rows `rows` of oracle.uniform((M, K), seed) on the host without the whole matrix: the counter generator of
+    oracle_uniform_at (qgemm_oracle.c), element i = row * K + col, U[-1, 1) = fl(fl(u - 0.5) * 2) (exact)."""
+    c = np.uint64(0x9E3779B97F4A7C15)
+
+    def mix64(z):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        key = mix64(np.uint64(seed) + c)
+        i = np.asarray(rows, np.uint64)[:, None] * np.uint64(K) + np.arange(K, dtype=np.uint64)[None, :]
+        z = mix64(key + (i + np.uint64(1)) * c)
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return (u + np.float32(-0.5)) * np.float32(2.0)
+
+
+def test_input_past_2_31_elements(qg, oracle, device):
+    """X of 600000 x 4096 (2.46e9 elements, 9.8 GB: input offsets past 2^31; packed A 2.46 GB) times a 4096 x 256 W:
+    sampled rows past the 2^31-th element of X, bit for bit against the oracle (each output row needs only its X row
+    and W's column scales).  The sampled X rows are regenerated on the host and checked against the device's first."""
+    M, N, K = 600000, 256, 4096
+    X = qg.fill_uniform(torch.empty((M, K), device=device), seed=2 * 59)
+    W = qg.fill_uniform(torch.empty((K, N), device=device), seed=2 * 59 + 1)
+    O = torch.full((M, N), float("nan"), device=device)
+    torch.cuda.synchronize()
+    assert qg.load().op_mm_quantize(X.data_ptr(), W.data_ptr(), O.data_ptr(), M, N, K) == 0
+    torch.cuda.synchronize()
+    first_past = (1 << 31) // K + 1
+    rows = np.unique(np.concatenate([[0, first_past - 1, first_past, M - 1],
+                                     np.linspace(first_past, M - 1, 28).astype(np.int64)]))
+    idx = torch.from_numpy(rows).to(device)
+    got, xdev = O[idx].cpu().numpy(), X[idx].cpu().numpy()
+    del O, X
+    Xs = _uniform_rows(2 * 59, rows, K)
+    assert_bits_equal(xdev, Xs, "X rows generation")
+    Wh = oracle.uniform((K, N), 2 * 59 + 1)
+    assert_bits_equal(got, oracle.quantized_mm_rows(Xs, Wh, np.arange(len(rows), dtype=np.int32)),
+                      f"{M}x{N}x{K} rows past 2^31 input elements")
+
+
 def test_strided_views(qg, oracle, device):
     """Transposed and sliced views, as the reference's Index() macro allows (tensor.cuh:121-149)."""
     M, N, K = 200, 150, 260
