@@ -79,7 +79,8 @@ def test_seeded_fixtures(qg, oracle, device):
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 768, 384), (1000, 300, 1030), (64, 4096, 256), (2048, 2048, 2048),
-                                   (64, 96, 5003), (33, 40, 16384), (300, 64, 8191)])  # long rows: block per row
+                                   (64, 96, 5003), (33, 40, 16384), (300, 64, 8191),   # long rows: block per row
+                                   (40, 72, 40000), (9, 24, 70001)])                   # past 16384: streaming rows
 def test_random_shapes_full_oracle(qg, oracle, device, M, N, K):
     X, W = oracle.inputs(M, N, K, 21)
     assert_bits_equal(_run_full(qg, X, W, device), oracle.quantized_mm(X, W), f"{M}x{N}x{K}")
