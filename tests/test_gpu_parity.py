@@ -328,6 +328,26 @@ def test_output_past_2_31_elements(qg, oracle, device):
     assert_bits_equal(got, oracle.quantized_mm_rows(Xh, Wh, rows.astype(np.int32)), f"{M}x{N}x{K} rows past 2^31")
 
 
+@pytest.mark.parametrize("M,N", [(0, 64), (64, 0), (0, 0)])
+def test_empty_output_is_a_no_op(qg, device, M, N):
+    """M = 0 or N = 0: nothing to compute -- the call returns 0 and touches no memory (the caller's buffers keep their
+    poison), through the flat entry point, the workspace form and the Python mirror."""
+    K = 32
+    X = torch.full((max(M, 1), K), 1.0, device=device)
+    W = torch.full((K, max(N, 1)), 1.0, device=device)
+    O = torch.full((8,), float("nan"), device=device)
+    L = qg.load()
+    torch.cuda.synchronize()
+    assert L.op_mm_quantize(X.data_ptr(), W.data_ptr(), O.data_ptr(), M, N, K) == 0
+    ws = torch.empty(max(1, L.op_mm_quantize_workspace_size(M, N, K)), dtype=torch.uint8, device=device)
+    assert L.op_mm_quantize_ws(X.data_ptr(), K, 1, W.data_ptr(), max(N, 1), 1, O.data_ptr(), max(N, 1), 1, M, N, K, 127.0,
+                               ws.data_ptr(), ws.numel(), None) == 0
+    out = qg.op_mm_quantize(X[:M], W[:, :N])
+    torch.cuda.synchronize()
+    assert tuple(out.shape) == (M, N)
+    assert torch.isnan(O).all()
+
+
 def _uniform_rows(seed, rows, K):
     """Rows `rows` of oracle.uniform((M, K), seed) on the host without the whole matrix: the counter generator of
     oracle_uniform_at (qgemm_oracle.c), element i = row * K + col, U[-1, 1) = fl(fl(u - 0.5) * 2) (exact)."""
